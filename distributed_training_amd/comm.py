@@ -1,0 +1,123 @@
+"""RCCL communicator owned by libgsync (one per process / GPU).
+
+The unique id is created on rank 0 and handed to the other ranks through the
+caller's ``torch.distributed`` process group (the same rendezvous the
+reference uses: ``init_process_group`` at R:resnet/pytorch_ddp/ddp_train.py:84),
+after which all gradient traffic goes through this communicator on its own
+high-priority stream — torch's ProcessGroupNCCL is only used for the
+bootstrap.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+
+_REDUCE_OPS = {"sum": L.GS_SUM, "prod": L.GS_PROD, "max": L.GS_MAX, "min": L.GS_MIN, "avg": L.GS_AVG}
+
+
+class Communicator:
+    def __init__(self, process_group=None, device: torch.device | None = None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if device.type != "cuda":
+            raise ValueError("Communicator needs a HIP device; CPU tensors use the gloo process group")
+        self.device = device
+        self.pg = process_group
+        self.rank = dist.get_rank(process_group)
+        self.world = dist.get_world_size(process_group)
+        lib = L.lib()
+        nbytes = lib.gs_comm_unique_id_bytes()
+        uid = (ctypes.c_uint8 * nbytes)()
+        if self.rank == 0:
+            L.check(lib.gs_comm_get_unique_id(uid), "gs_comm_get_unique_id")
+        obj = [bytes(uid)]
+        group_src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        dist.broadcast_object_list(obj, src=group_src, group=process_group, device=self._bootstrap_device())
+        uid = (ctypes.c_uint8 * nbytes).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(device)
+        L.check(lib.gs_comm_create(self.rank, self.world, uid, device.index, ctypes.byref(h)), "gs_comm_create")
+        self.handle = h
+        s = ctypes.c_void_p()
+        L.check(lib.gs_comm_stream(h, ctypes.byref(s)), "gs_comm_stream")
+        self.stream_ptr = s.value
+        self.stream = torch.cuda.ExternalStream(self.stream_ptr, device=device)
+
+    def _bootstrap_device(self):
+        backend = dist.get_backend(self.pg)
+        return self.device if backend in ("nccl", "rccl") else torch.device("cpu")
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            L.lib().gs_comm_destroy(h)
+            self.handle = None
+
+    def abort(self):
+        if self.handle is not None:
+            L.check(L.lib().gs_comm_abort(self.handle), "gs_comm_abort")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    # ------------------------------------------------------------ collectives
+    def _s(self, stream):
+        return self.stream_ptr if stream is None else stream
+
+    def all_reduce(self, t: torch.Tensor, op="sum", stream=None, out: torch.Tensor | None = None):
+        out = t if out is None else out
+        L.check(L.lib().gs_allreduce(self.handle, t.data_ptr(), out.data_ptr(), t.numel(), L.gs_dtype(t.dtype),
+                                     _REDUCE_OPS[op], self._s(stream)), "gs_allreduce")
+        return out
+
+    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, op="sum", stream=None):
+        L.check(L.lib().gs_reduce_scatter(self.handle, send.data_ptr(), recv.data_ptr(), recv.numel(),
+                                          L.gs_dtype(send.dtype), _REDUCE_OPS[op], self._s(stream)),
+                "gs_reduce_scatter")
+        return recv
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream=None):
+        L.check(L.lib().gs_all_gather(self.handle, send.data_ptr(), recv.data_ptr(), send.numel(),
+                                      L.gs_dtype(send.dtype), self._s(stream)), "gs_all_gather")
+        return recv
+
+    def broadcast(self, t: torch.Tensor, root=0, stream=None):
+        L.check(L.lib().gs_broadcast(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), L.gs_dtype(t.dtype),
+                                     root, self._s(stream)), "gs_broadcast")
+        return t
+
+    def wait_on_current(self):
+        """comm stream waits for everything queued on torch's current stream."""
+        L.check(L.lib().gs_stream_wait(self.stream_ptr, L.stream_ptr(self.device)), "gs_stream_wait")
+
+    def current_waits(self):
+        """torch's current stream waits for everything queued on the comm stream."""
+        L.check(L.lib().gs_stream_wait(L.stream_ptr(self.device), self.stream_ptr), "gs_stream_wait")
+
+
+_COMMS: dict = {}
+
+
+def get_communicator(process_group=None, device=None) -> Communicator:
+    """Process-wide cache: one communicator per (group, device)."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (id(process_group) if process_group is not None else None, device.index)
+    c = _COMMS.get(key)
+    if c is None:
+        c = Communicator(process_group, device)
+        _COMMS[key] = c
+    return c
+
+
+def destroy_communicators():
+    for c in list(_COMMS.values()):
+        c.close()
+    _COMMS.clear()

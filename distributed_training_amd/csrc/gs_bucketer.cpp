@@ -1,0 +1,405 @@
+// libgsync bucketer: the Reducer state machine of torch DDP restated for
+// MI355X (T:include/torch/csrc/distributed/c10d/reducer.hpp:52-63 ctor,
+// :73 autograd_hook, :275 mark_variable_ready_dense, :111-116 run_comm_hook,
+// :283 finalize_bucket_dense, :346-402 Bucket).
+//
+// Differences in HOW (not WHAT):
+//  - a bucket is packed by ONE multi-tensor launch when its last gradient is
+//    ready (torch: one elementwise launch per parameter, 161 for ResNet-50);
+//  - pack, collective and unpack all run on the communicator's own stream,
+//    ordered after the producer (autograd) stream by one event, so the whole
+//    per-bucket chain overlaps the rest of backward and only the last
+//    bucket's chain is exposed;
+//  - per-parameter offsets inside a bucket are padded to `align_elems` so
+//    every access is a full 16-B vector access; padding is zero and is
+//    reduced as zero.
+// Buckets launch strictly in index order (next_bucket_), so every rank issues
+// the same collective sequence, as Reducer::mark_bucket_ready does.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <mutex>
+
+#include "gs_common.h"
+
+namespace gs {
+ncclComm_t comm_handle(gs_comm* c);
+hipStream_t comm_stream(gs_comm* c);
+int comm_dtype(int dt, ncclDataType_t* out);
+}  // namespace gs
+
+using namespace gs;
+
+namespace {
+
+#define HIPB_RET(expr)                                                               \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      return fail(GS_EHIP, std::string(#expr " failed: ") + hipGetErrorString(_e));  \
+  } while (0)
+
+struct Bucket {
+  std::vector<int32_t> params;  // global parameter ids, bucket order
+  gs_plan* plan = nullptr;      // layout of the params inside the flat bucket
+  gs_plan* flat = nullptr;      // the whole flat bucket as one tensor (in-place ops)
+  int64_t numel = 0;            // padded flat numel
+  void* buf = nullptr;          // torch-owned flat storage
+  void* shard = nullptr;        // torch-owned reduce-scatter output
+  int pending = 0;
+  bool launched = false;
+  bool unpacked = false;
+  hipEvent_t ev_ready = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+  bool timed = false;
+};
+
+}  // namespace
+
+struct gs_bucketer {
+  gs_comm* comm = nullptr;
+  int kind = GS_DEV_HOST;
+  int device = 0;
+  int n_params = 0;
+  int grad_dtype = GS_F32;
+  int bucket_dtype = GS_F32;
+  int64_t align = 0;
+  float div = 1.f;
+  int flags = 0;
+  std::vector<Bucket> buckets;
+  std::vector<int32_t> loc_bucket, loc_intra;
+  std::vector<int64_t> numel;
+  std::vector<char> ready;
+  int next_bucket = 0;
+  bool prepared = false;
+  float* sqnorm = nullptr;
+  int sq_count = 0;
+  void* producer = nullptr;
+  hipEvent_t ev_done = nullptr;
+  std::mutex mu;
+
+  bool hip() const { return kind == GS_DEV_HIP; }
+  bool auto_coll() const { return (flags & GS_BKT_AUTO_COLLECTIVE) != 0; }
+  bool do_unpack() const {
+    return (flags & (GS_BKT_GRAD_VIEW | GS_BKT_NO_UNPACK | GS_BKT_REDUCE_SCATTER)) == 0;
+  }
+};
+
+namespace {
+
+void plan_set_one(gs_plan* p, int slot, int t, void* ptr) {
+  void*& cur = p->h_ptrs[static_cast<size_t>(slot) * p->n + t];
+  if (cur == ptr) return;
+  cur = ptr;
+  const uint32_t bit = 1u << slot;
+  const bool al = (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0;
+  p->h_align[t] = al ? (p->h_align[t] | bit) : (p->h_align[t] & ~bit);
+  p->dirty = true;
+}
+
+int unpack_one(gs_bucketer* b, Bucket& bk, void* stream, int accumulate_sq) {
+  float* sq = b->sqnorm;
+  const int acc = (b->sq_count > 0 || accumulate_sq) ? 1 : 0;
+  GS_TRY_RET(gs_unpack(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, sq, acc, stream));
+  if (sq) ++b->sq_count;
+  bk.unpacked = true;
+  return GS_OK;
+}
+
+// pack (or scale in place) bucket bk on `stream`
+int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
+  const bool no_scale = (b->flags & GS_BKT_NO_SCALE) != 0;
+  if (b->flags & GS_BKT_GRAD_VIEW) {
+    // grads alias the bucket (gradient_as_bucket_view): bucket_view.div_(div_factor)
+    bool all_alias = true;
+    const int es = dtype_size(b->bucket_dtype);
+    for (size_t i = 0; i < bk.params.size(); ++i) {
+      const void* g = bk.plan->h_ptrs[static_cast<size_t>(1) * bk.plan->n + i];
+      if (g != static_cast<char*>(bk.buf) + bk.plan->off[i] * es) { all_alias = false; break; }
+    }
+    if (all_alias) {
+      if (no_scale || b->div == 1.f) return GS_OK;
+      return gs_scale(bk.flat, 0, b->bucket_dtype, b->div, GS_SCALE_DIV, stream);
+    }
+  }
+  if (no_scale) return gs_pack(bk.plan, 1, b->grad_dtype, bk.buf, b->bucket_dtype, 1.f, GS_SCALE_NONE, stream);
+  // at::mul_out(bucket_view, grad, 1/div_factor): the scalar is float(1.0/div)
+  const float inv = static_cast<float>(1.0 / static_cast<double>(b->div));
+  return gs_pack(bk.plan, 1, b->grad_dtype, bk.buf, b->bucket_dtype, inv, GS_SCALE_MUL, stream);
+}
+
+int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
+  ncclDataType_t dt;
+  GS_TRY_RET(comm_dtype(b->bucket_dtype, &dt));
+  ncclResult_t r;
+  if (b->flags & GS_BKT_REDUCE_SCATTER) {
+    const int w = gs_comm_world(b->comm);
+    r = ncclReduceScatter(bk.buf, bk.shard, static_cast<size_t>(bk.numel / w), dt, ncclSum,
+                          comm_handle(b->comm), cs);
+  } else {
+    r = ncclAllReduce(bk.buf, bk.buf, static_cast<size_t>(bk.numel), dt, ncclSum,
+                      comm_handle(b->comm), cs);
+  }
+  if (r != ncclSuccess) return fail(GS_ERCCL, std::string("bucket collective: ") + ncclGetErrorString(r));
+  return GS_OK;
+}
+
+int launch_bucket(gs_bucketer* b, int bi) {
+  Bucket& bk = b->buckets[bi];
+  if (!bk.buf) return fail(GS_ESTATE, "bucket " + std::to_string(bi) + " has no storage");
+  if (!b->hip()) {
+    GS_TRY_RET(pack_one(b, bk, nullptr));
+  } else if (b->auto_coll()) {
+    hipStream_t cs = comm_stream(b->comm);
+    HIPB_RET(hipEventRecord(bk.ev_ready, static_cast<hipStream_t>(b->producer)));
+    HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
+    GS_TRY_RET(pack_one(b, bk, cs));
+    HIPB_RET(hipEventRecord(bk.ev_t0, cs));
+    GS_TRY_RET(launch_collective(b, bk, cs));
+    HIPB_RET(hipEventRecord(bk.ev_t1, cs));
+    bk.timed = true;
+    if (b->do_unpack()) GS_TRY_RET(unpack_one(b, bk, cs, 0));
+  } else {
+    GS_TRY_RET(pack_one(b, bk, b->producer));
+  }
+  bk.launched = true;
+  return GS_OK;
+}
+
+int drain_ready(gs_bucketer* b, int32_t* ready_out, int32_t* n_ready) {
+  int nr = 0;
+  while (b->next_bucket < static_cast<int>(b->buckets.size()) &&
+         b->buckets[b->next_bucket].pending == 0) {
+    GS_TRY_RET(launch_bucket(b, b->next_bucket));
+    if (ready_out) ready_out[nr] = b->next_bucket;
+    ++nr;
+    ++b->next_bucket;
+  }
+  if (n_ready) *n_ready = nr;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
+                       const int64_t* numels, int grad_dtype, int n_buckets,
+                       const int32_t* bucket_counts, const int32_t* bucket_members,
+                       int bucket_dtype, int64_t align_elems, float div_factor, int flags,
+                       gs_bucketer** out) {
+  GS_CHECK_ARG(out && numels && bucket_counts && bucket_members, "gs_bucketer_create: NULL argument");
+  GS_CHECK_ARG(n_params >= 0 && n_buckets >= 0, "gs_bucketer_create: negative count");
+  GS_CHECK_ARG(is_float_dtype(grad_dtype) && is_float_dtype(bucket_dtype),
+               "gs_bucketer_create: grad and bucket dtypes must be floating");
+  GS_CHECK_ARG(div_factor > 0.f, "gs_bucketer_create: div_factor must be > 0");
+  GS_CHECK_ARG(!(flags & GS_BKT_AUTO_COLLECTIVE) || (comm && device_kind == GS_DEV_HIP),
+               "gs_bucketer_create: AUTO_COLLECTIVE needs a HIP communicator");
+  GS_CHECK_ARG(!(flags & GS_BKT_REDUCE_SCATTER) || comm,
+               "gs_bucketer_create: REDUCE_SCATTER needs a communicator");
+  auto* b = new gs_bucketer();
+  b->comm = comm;
+  b->kind = device_kind;
+  b->device = device;
+  b->n_params = n_params;
+  b->grad_dtype = grad_dtype;
+  b->bucket_dtype = bucket_dtype;
+  b->align = align_elems;
+  b->div = div_factor;
+  b->flags = flags;
+  b->numel.assign(numels, numels + n_params);
+  b->loc_bucket.assign(n_params, -1);
+  b->loc_intra.assign(n_params, -1);
+  b->ready.assign(n_params, 0);
+  b->buckets.resize(n_buckets);
+  int pos = 0;
+  auto bail = [&](int rc) {
+    gs_bucketer_destroy(b);
+    return rc;
+  };
+  const int world = comm ? gs_comm_world(comm) : 1;
+  for (int bi = 0; bi < n_buckets; ++bi) {
+    Bucket& bk = b->buckets[bi];
+    std::vector<int64_t> nm;
+    for (int k = 0; k < bucket_counts[bi]; ++k) {
+      const int32_t p = bucket_members[pos++];
+      if (p < 0 || p >= n_params || b->loc_bucket[p] != -1)
+        return bail(fail(GS_EINVAL, "gs_bucketer_create: bad or duplicate member " + std::to_string(p)));
+      b->loc_bucket[p] = bi;
+      b->loc_intra[p] = k;
+      bk.params.push_back(p);
+      nm.push_back(numels[p]);
+    }
+    int rc = gs_plan_create(device_kind, device, static_cast<int>(nm.size()), nm.data(), align_elems, &bk.plan);
+    if (rc != GS_OK) return bail(rc);
+    bk.numel = bk.plan->flat_numel;
+    if (flags & GS_BKT_REDUCE_SCATTER) {
+      // pad so the bucket splits into `world` equal, aligned shards
+      const int64_t q = static_cast<int64_t>(world) * (align_elems > 0 ? align_elems : 1);
+      bk.numel = (bk.numel + q - 1) / q * q;
+    }
+    rc = gs_plan_create(device_kind, device, 1, &bk.numel, 0, &bk.flat);
+    if (rc != GS_OK) return bail(rc);
+    bk.pending = static_cast<int>(bk.params.size());
+    if (device_kind == GS_DEV_HIP) {
+      if (hipEventCreateWithFlags(&bk.ev_ready, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess)
+        return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
+    }
+  }
+  for (int p = 0; p < n_params; ++p)
+    if (b->loc_bucket[p] < 0)
+      return bail(fail(GS_EINVAL, "gs_bucketer_create: parameter " + std::to_string(p) + " is in no bucket"));
+  if (device_kind == GS_DEV_HIP &&
+      hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
+  *out = b;
+  return GS_OK;
+}
+
+int gs_bucketer_destroy(gs_bucketer* b) {
+  if (!b) return GS_OK;
+  if (b->hip() && b->comm) (void)hipStreamSynchronize(comm_stream(b->comm));
+  for (Bucket& bk : b->buckets) {
+    gs_plan_destroy(bk.plan);
+    gs_plan_destroy(bk.flat);
+    if (bk.ev_ready) (void)hipEventDestroy(bk.ev_ready);
+    if (bk.ev_t0) (void)hipEventDestroy(bk.ev_t0);
+    if (bk.ev_t1) (void)hipEventDestroy(bk.ev_t1);
+  }
+  if (b->ev_done) (void)hipEventDestroy(b->ev_done);
+  delete b;
+  return GS_OK;
+}
+
+int gs_bucketer_bucket_numel(gs_bucketer* b, int bucket, int64_t* out) {
+  GS_CHECK_ARG(b && out && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  *out = b->buckets[bucket].numel;
+  return GS_OK;
+}
+
+int gs_bucketer_shard_numel(gs_bucketer* b, int bucket, int64_t* out) {
+  GS_CHECK_ARG(b && out && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  const int w = b->comm ? gs_comm_world(b->comm) : 1;
+  *out = b->buckets[bucket].numel / w;
+  return GS_OK;
+}
+
+int gs_bucketer_param_location(gs_bucketer* b, int param, int32_t* bucket, int64_t* offset) {
+  GS_CHECK_ARG(b && param >= 0 && param < b->n_params, "gs_bucketer_param_location: bad param");
+  const int bi = b->loc_bucket[param];
+  if (bucket) *bucket = bi;
+  if (offset) *offset = b->buckets[bi].plan->off[b->loc_intra[param]];
+  return GS_OK;
+}
+
+int gs_bucketer_set_bucket_buffer(gs_bucketer* b, int bucket, void* ptr) {
+  GS_CHECK_ARG(b && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  GS_CHECK_ARG(ptr != nullptr, "gs_bucketer_set_bucket_buffer: NULL storage");
+  Bucket& bk = b->buckets[bucket];
+  bk.buf = ptr;
+  void* one[1] = {ptr};
+  return gs_plan_set_ptrs(bk.flat, 0, one, nullptr);
+}
+
+int gs_bucketer_set_shard_buffer(gs_bucketer* b, int bucket, void* ptr) {
+  GS_CHECK_ARG(b && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  b->buckets[bucket].shard = ptr;
+  return GS_OK;
+}
+
+int gs_bucketer_prepare(gs_bucketer* b, float* sqnorm_dev) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_prepare: NULL bucketer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  std::fill(b->ready.begin(), b->ready.end(), 0);
+  for (Bucket& bk : b->buckets) {
+    bk.pending = static_cast<int>(bk.params.size());
+    bk.launched = false;
+    bk.unpacked = false;
+  }
+  b->next_bucket = 0;
+  b->prepared = true;
+  b->sqnorm = sqnorm_dev;
+  b->sq_count = 0;
+  b->producer = nullptr;
+  return GS_OK;
+}
+
+int gs_bucketer_mark_ready(gs_bucketer* b, int param, const void* grad, void* stream,
+                           int32_t* ready_out, int32_t* n_ready) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_mark_ready: NULL bucketer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (n_ready) *n_ready = 0;
+  if (!b->prepared)
+    return fail(GS_ESTATE, "mark_ready called outside of a synchronising backward (prepare not called)");
+  GS_CHECK_ARG(param >= 0 && param < b->n_params, "gs_bucketer_mark_ready: param out of range");
+  if (b->ready[param])
+    return fail(GS_ESTATE, "Expected to mark a variable ready only once. Parameter " +
+                               std::to_string(param) + " was marked twice in one backward.");
+  b->ready[param] = 1;
+  if (b->producer == nullptr) b->producer = stream;
+  Bucket& bk = b->buckets[b->loc_bucket[param]];
+  plan_set_one(bk.plan, 1, b->loc_intra[param], const_cast<void*>(grad));
+  bk.pending -= 1;
+  return drain_ready(b, ready_out, n_ready);
+}
+
+int gs_bucketer_mark_unused(gs_bucketer* b, void* stream, int32_t* ready_out, int32_t* n_ready) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_mark_unused: NULL bucketer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (!b->prepared) return fail(GS_ESTATE, "mark_unused outside of a synchronising backward");
+  if (b->producer == nullptr) b->producer = stream;
+  for (int p = 0; p < b->n_params; ++p) {
+    if (b->ready[p]) continue;
+    b->ready[p] = 1;
+    Bucket& bk = b->buckets[b->loc_bucket[p]];
+    // a NULL source packs zeros and a NULL destination is skipped by unpack
+    plan_set_one(bk.plan, 1, b->loc_intra[p], nullptr);
+    bk.pending -= 1;
+  }
+  return drain_ready(b, ready_out, n_ready);
+}
+
+int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_finalize: NULL bucketer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (!b->prepared) return fail(GS_ESTATE, "finalize without prepare");
+  if (b->next_bucket != static_cast<int>(b->buckets.size())) {
+    std::string missing;
+    int shown = 0;
+    for (int p = 0; p < b->n_params && shown < 16; ++p)
+      if (!b->ready[p]) { missing += (shown ? ", " : "") + std::to_string(p); ++shown; }
+    return fail(GS_ESTATE,
+                "Expected to have finished reduction in the prior iteration before starting a new "
+                "one. Parameter indices which did not receive grad: " + missing);
+  }
+  if (b->hip() && b->auto_coll()) {
+    hipStream_t cs = comm_stream(b->comm);
+    HIPB_RET(hipEventRecord(b->ev_done, cs));
+    HIPB_RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), b->ev_done, 0));
+  } else if (b->do_unpack()) {
+    for (Bucket& bk : b->buckets)
+      if (!bk.unpacked) GS_TRY_RET(unpack_one(b, bk, stream, 0));
+  }
+  b->prepared = false;
+  return GS_OK;
+}
+
+int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream) {
+  GS_CHECK_ARG(b && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  std::lock_guard<std::mutex> lk(b->mu);
+  Bucket& bk = b->buckets[bucket];
+  if (!bk.launched) return fail(GS_ESTATE, "unpack of a bucket that was never launched");
+  return unpack_one(b, bk, stream, 0);
+}
+
+int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms) {
+  GS_CHECK_ARG(b && ms && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  Bucket& bk = b->buckets[bucket];
+  *ms = -1.f;
+  if (!bk.timed) return GS_OK;
+  HIPB_RET(hipEventSynchronize(bk.ev_t1));
+  HIPB_RET(hipEventElapsedTime(ms, bk.ev_t0, bk.ev_t1));
+  return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,159 @@
+// Internal declarations shared by the libgsync translation units.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gsync.h"
+
+namespace gs {
+
+// ---- error plumbing: thread-local message, int codes across the ABI ----
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define GS_CHECK_ARG(cond, msg)                                   \
+  do {                                                            \
+    if (!(cond)) return ::gs::fail(GS_EINVAL, std::string(msg));  \
+  } while (0)
+
+#define GS_TRY_RET(expr)          \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != GS_OK) return _rc; \
+  } while (0)
+
+inline int dtype_size(int dt) {
+  switch (dt) {
+    case GS_F32: return 4;
+    case GS_BF16: return 2;
+    case GS_F16: return 2;
+    case GS_F64: return 8;
+    case GS_I64: return 8;
+    case GS_I32: return 4;
+    case GS_U8: return 1;
+    default: return 0;
+  }
+}
+inline bool is_float_dtype(int dt) { return dt == GS_F32 || dt == GS_BF16 || dt == GS_F16; }
+
+// ---- multi-tensor work decomposition ----
+// A tensor is cut into segments of <= kSegUnits units (1 unit = 4 elements).
+// Consecutive segments are grouped into tasks of <= kTaskUnits units and
+// <= kMaxSegPerTask segments; one workgroup processes one task at a time
+// (small tensors share a task; their descriptors are staged in LDS).
+constexpr int kUnit = 4;
+constexpr int kSegUnits = 4096;     // 16Ki elements = 64 KiB fp32 per stream
+constexpr int kTaskUnits = 4096;
+constexpr int kMaxSegPerTask = 64;
+constexpr int kBlock = 256;         // 4 waves of 64
+constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups
+
+struct Seg {
+  int64_t unit_begin;  // first unit inside the tensor
+  int32_t tensor;
+  int32_t units;
+  int32_t task_off;    // unit offset of this segment inside its task
+  int32_t pad;
+};
+static_assert(sizeof(Seg) == 24, "Seg layout");
+
+// Arguments handed to a device kernel (by value).
+struct PlanArgs {
+  const Seg* segs;
+  const int32_t* task_begin;  // [n_tasks + 1]
+  const int64_t* numel;       // [n]
+  const int64_t* off;         // [n] flat offsets (elements)
+  void* const* ptrs;          // [GS_PLAN_SLOTS * n]
+  const uint32_t* align;      // [n] bit s = slot s pointer is 16-B aligned
+  int32_t n;
+  int32_t n_tasks;
+};
+
+// optimizer hyper-parameters, rounded to fp32 where torch rounds them
+struct SgdHyper {
+  float lr, mom, omd, wd;  // omd = float(1 - dampening) formed in double
+  int nesterov, maximize, first;
+};
+struct AdamHyper {
+  float b2, w1, w2, eps, wd, step_size, bc2s, decay;  // w1 = float(1-b1), decay = float(1-lr*wd)
+  int adamw, maximize;
+};
+inline SgdHyper make_sgd(double lr, double mom, double damp, double wd, int nest, int maxi,
+                         int first) {
+  return SgdHyper{static_cast<float>(lr), static_cast<float>(mom),
+                  static_cast<float>(1.0 - damp), static_cast<float>(wd), nest, maxi, first};
+}
+inline AdamHyper make_adam(double lr, double b1, double b2, double eps, double wd, int adamw,
+                           int maxi, double step_size, double bc2s) {
+  return AdamHyper{static_cast<float>(b2), static_cast<float>(1.0 - b1),
+                   static_cast<float>(1.0 - b2), static_cast<float>(eps),
+                   static_cast<float>(wd), static_cast<float>(step_size),
+                   static_cast<float>(bc2s), static_cast<float>(1.0 - lr * wd), adamw, maxi};
+}
+
+}  // namespace gs
+
+// The opaque plan (visible to every TU of the library).
+struct gs_plan {
+  int kind = GS_DEV_HOST;
+  int device = 0;
+  int n = 0;
+  int64_t align_elems = 0;
+  int64_t flat_numel = 0;
+  std::vector<int64_t> numel, off;
+  std::vector<gs::Seg> segs;
+  std::vector<int32_t> task_begin;
+  int grid = 0;
+  // host shadow of the pointer table
+  std::vector<void*> h_ptrs;       // [SLOTS * n]
+  std::vector<uint32_t> h_align;   // [n]
+  bool dirty = true;
+  // device side (HIP plans only)
+  void* d_static = nullptr;  // segs | task_begin | numel | off
+  void* d_table = nullptr;   // ptrs | align
+  float* d_partials = nullptr;  // [kMaxGrid]
+  void* pinned = nullptr;       // staging ring for table uploads
+  int ring = 0;
+  void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* last_stream = nullptr;
+  void* last_event = nullptr;
+  gs::PlanArgs args() const;
+};
+
+namespace gs {
+// HIP-side implementations (gs_kernels.hip)
+int hip_plan_upload_static(gs_plan* p);
+int hip_plan_release(gs_plan* p);
+int hip_plan_flush(gs_plan* p, void* stream);
+int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
+             void* stream);
+int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
+               int acc, void* stream);
+int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream);
+int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream);
+int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm,
+                  void* stream);
+int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
+                      void* stream);
+int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi,
+            void* stream);
+int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs, const float* fi,
+             void* stream);
+int hip_device_count();
+int hip_memset_async(void* dst, int value, size_t bytes, void* stream);
+int hip_stream_wait(void* waiter, void* signaler);
+
+// host-side implementations (gs_host.cpp)
+int host_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode);
+int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
+                int acc);
+int host_scale(gs_plan* p, int slot, int dt, float s, int mode);
+int host_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc);
+int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm);
+int host_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found);
+int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi);
+int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs, const float* fi);
+}  // namespace gs

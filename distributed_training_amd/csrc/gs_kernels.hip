@@ -1,0 +1,729 @@
+// gfx950 (CDNA4) kernels of libgsync: multi-tensor pack / unpack / scale /
+// sq-norm / unscale and the fused SGD / Adam updates.
+//
+// All of them are HBM-streaming kernels (no MFMA: nothing here is a
+// contraction).  One work decomposition serves every op: a plan cuts each
+// tensor into 4-element units, units into segments (<= 16 Ki elements) and
+// segments into tasks (<= 16 Ki elements, <= 64 segments).  A 256-thread
+// workgroup (4 wave64) takes one task at a time; the task's segment
+// descriptors are staged in LDS so that a workgroup gathers many small
+// tensors (BN weights/biases, 1x1-conv biases ...) in one pass with every
+// lane busy, while a large tensor gets one segment per task.  Every lane
+// moves 4 elements per access (16 B for fp32, 8 B for bf16/fp16) with ILP
+// accesses in flight before the first use.
+//
+// Arithmetic is written with explicit fmaf and compiled with
+// -ffp-contract=off so that the host restatement (oracle/gs_oracle.c) and
+// the host backend (gs_host.cpp) reproduce it bit for bit.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+
+#include "gs_common.h"
+
+namespace gs {
+
+namespace {
+
+#define HIP_RET(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(GS_EHIP, std::string(#expr " failed: ") + hipGetErrorString(_e));   \
+  } while (0)
+
+// ---------------------------------------------------------------- dtype I/O
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+// round-to-nearest-even; NaN -> 0x7FC0 (c10::BFloat16 round_to_nearest_even)
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7FC0;
+  return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  _Float16 x;
+  __builtin_memcpy(&x, &h, 2);
+  return static_cast<float>(x);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  _Float16 x = static_cast<_Float16>(f);
+  uint16_t h;
+  __builtin_memcpy(&h, &x, 2);
+  return h;
+}
+
+template <int DT>
+__device__ __forceinline__ float to_f32(uint16_t h) {
+  if constexpr (DT == GS_BF16) return bf16_to_f32(h);
+  else return f16_to_f32(h);
+}
+template <int DT>
+__device__ __forceinline__ uint16_t from_f32(float f) {
+  if constexpr (DT == GS_BF16) return f32_to_bf16(f);
+  else return f32_to_f16(f);
+}
+// value as it would read back after a store in DT (used for norms / casts)
+template <int DT>
+__device__ __forceinline__ float round_to(float f) {
+  if constexpr (DT == GS_F32) return f;
+  else return to_f32<DT>(from_f32<DT>(f));
+}
+
+// Plan pointers are read from a table, so the compiler only sees generic
+// pointers and would emit flat_* accesses; every buffer here is device
+// global memory, so accesses go through address_space(1) (global_*) with
+// native 16-B / 8-B vector types.
+typedef float gf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t gu2 __attribute__((ext_vector_type(2)));
+#define GLOBAL_AS __attribute__((address_space(1)))
+
+template <class T>
+__device__ __forceinline__ const GLOBAL_AS T* gptr(const void* p) {
+  return (const GLOBAL_AS T*)(p);
+}
+template <class T>
+__device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
+  return (GLOBAL_AS T*)(p);
+}
+
+// load 4 consecutive elements [e, e+4) of a tensor with n elements
+template <int DT>
+__device__ __forceinline__ void load4(const void* base, int64_t e, int64_t n, bool vec,
+                                      float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    const GLOBAL_AS float* p = gptr<float>(base) + e;
+    if (vec && e + 4 <= n) {
+      const gf4 v = *(const GLOBAL_AS gf4*)p;
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = (e + i < n) ? p[i] : 0.f;
+    }
+  } else {
+    const GLOBAL_AS uint16_t* p = gptr<uint16_t>(base) + e;
+    if (vec && e + 4 <= n) {
+      const gu2 v = *(const GLOBAL_AS gu2*)p;
+      x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
+      x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
+      x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
+      x[3] = to_f32<DT>(static_cast<uint16_t>(v.y >> 16));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = (e + i < n) ? to_f32<DT>(p[i]) : 0.f;
+    }
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void store4(void* base, int64_t e, int64_t n, bool vec,
+                                       const float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    GLOBAL_AS float* p = gptr_w<float>(base) + e;
+    if (vec && e + 4 <= n) {
+      gf4 v;
+      v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
+      *(GLOBAL_AS gf4*)p = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (e + i < n) p[i] = x[i];
+    }
+  } else {
+    GLOBAL_AS uint16_t* p = gptr_w<uint16_t>(base) + e;
+    if (vec && e + 4 <= n) {
+      gu2 v;
+      v.x = static_cast<uint32_t>(from_f32<DT>(x[0])) |
+            (static_cast<uint32_t>(from_f32<DT>(x[1])) << 16);
+      v.y = static_cast<uint32_t>(from_f32<DT>(x[2])) |
+            (static_cast<uint32_t>(from_f32<DT>(x[3])) << 16);
+      *(GLOBAL_AS gu2*)p = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (e + i < n) p[i] = from_f32<DT>(x[i]);
+    }
+  }
+}
+
+__device__ __forceinline__ void* slot_ptr(const PlanArgs& P, int slot, int t) {
+  return P.ptrs[static_cast<int64_t>(slot) * P.n + t];
+}
+__device__ __forceinline__ bool slot_vec(const PlanArgs& P, int slot, int t) {
+  return (P.align[t] >> slot) & 1u;
+}
+
+// ------------------------------------------------------- wave/block reduce
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// block of kBlock threads; result valid in thread 0
+template <bool MAX>
+__device__ __forceinline__ float block_reduce(float v) {
+  __shared__ float s_red[kBlock / 64];
+  v = MAX ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) s_red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0) {
+    r = s_red[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; ++i) r = MAX ? fmaxf(r, s_red[i]) : r + s_red[i];
+  }
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------- the engine
+// Op contract:
+//   struct Frag;                          registers for one unit
+//   bool active() const;                  uniform early-out (found_inf skip)
+//   void load(P, t, e, Frag&)             issue the unit's loads
+//   void apply(P, t, e, Frag&, float& acc) compute + store (+ reduction)
+//   static constexpr int kRed = 0 (none) | 1 (sum) | 2 (max); float* partials
+template <int ILP, class Op>
+__global__ void __launch_bounds__(kBlock) mt_kernel(PlanArgs P, Op op) {
+  __shared__ int32_t s_tensor[kMaxSegPerTask];
+  __shared__ int64_t s_ubeg[kMaxSegPerTask];
+  __shared__ int32_t s_pref[kMaxSegPerTask + 1];
+  float acc = 0.f;
+  if (!op.active()) return;  // uniform across the grid
+  for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
+    const int sb = P.task_begin[task];
+    const int ns = P.task_begin[task + 1] - sb;
+    if (threadIdx.x < ns) {
+      const Seg sg = P.segs[sb + threadIdx.x];
+      s_tensor[threadIdx.x] = sg.tensor;
+      s_ubeg[threadIdx.x] = sg.unit_begin;
+      s_pref[threadIdx.x] = sg.task_off;
+      if (threadIdx.x == ns - 1) s_pref[ns] = sg.task_off + sg.units;
+    }
+    __syncthreads();
+    const int total = s_pref[ns];
+    for (int base = 0; base < total; base += kBlock * ILP) {
+      typename Op::Frag f[ILP];
+      int tt[ILP];
+      int64_t ee[ILP];
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+        tt[j] = -1;
+        if (u < total) {
+          int k = 0;
+          if (ns > 1) {  // binary search in the LDS-staged prefix
+            int lo = 0, hi = ns - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (s_pref[mid] <= u) lo = mid; else hi = mid - 1;
+            }
+            k = lo;
+          }
+          tt[j] = s_tensor[k];
+          ee[j] = (s_ubeg[k] + (u - s_pref[k])) * kUnit;
+          op.load(P, tt[j], ee[j], f[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < ILP; ++j)
+        if (tt[j] >= 0) op.apply(P, tt[j], ee[j], f[j], acc);
+    }
+    __syncthreads();
+  }
+  if constexpr (Op::kRed != 0) {
+    const float r = block_reduce<Op::kRed == 2>(acc);
+    if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+  }
+}
+
+// deterministic combine of the per-workgroup partials (fixed order)
+template <bool MAX>
+__global__ void __launch_bounds__(kBlock) combine_partials(const float* partials, int n,
+                                                           float* out, int accumulate) {
+  float v = 0.f;
+  for (int i = threadIdx.x; i < n; i += kBlock)
+    v = MAX ? fmaxf(v, partials[i]) : v + partials[i];
+  const float r = block_reduce<MAX>(v);
+  if (threadIdx.x == 0) {
+    if (MAX) out[0] = accumulate ? fmaxf(out[0], r) : r;
+    else out[0] = accumulate ? out[0] + r : r;
+  }
+}
+
+// ---------------------------------------------------------------- ops
+template <int SD, int FD>
+struct PackOp {
+  static constexpr int kRed = 0;
+  float* partials = nullptr;
+  int slot;
+  void* flat;
+  bool flat_vec;
+  float s;
+  int mode;
+  struct Frag { float x[4]; };
+  __device__ bool active() const { return true; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    const void* src = slot_ptr(P, slot, t);
+    if (src == nullptr) {  // unused parameter (find_unused_parameters): pack zeros
+      f.x[0] = f.x[1] = f.x[2] = f.x[3] = 0.f;
+      return;
+    }
+    load4<SD>(src, e, P.numel[t], slot_vec(P, slot, t), f.x);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
+    const int64_t off = P.off[t];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = f.x[i];
+      if (mode == GS_SCALE_MUL) {
+        v = v * s;
+      } else if (mode == GS_SCALE_DIV) {
+        // bf16_compress_hook order: round to the bucket dtype, then divide
+        v = round_to<FD>(v) / s;
+      }
+      f.x[i] = v;
+    }
+    char* fb = static_cast<char*>(flat) + off * (FD == GS_F32 ? 4 : 2);
+    store4<FD>(fb, e, P.numel[t], flat_vec && (off % kUnit) == 0, f.x);
+  }
+};
+
+template <int FD, int DD>
+struct UnpackOp {
+  static constexpr int kRed = 1;
+  float* partials = nullptr;
+  bool want_sq;
+  const void* flat;
+  bool flat_vec;
+  int slot;
+  struct Frag { float x[4]; };
+  __device__ bool active() const { return true; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    const int64_t off = P.off[t];
+    const char* fb = static_cast<const char*>(flat) + off * (FD == GS_F32 ? 4 : 2);
+    load4<FD>(fb, e, P.numel[t], flat_vec && (off % kUnit) == 0, f.x);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float& acc) const {
+    void* dst = slot_ptr(P, slot, t);
+    if (dst == nullptr) return;  // unused parameter: grad left untouched
+    store4<DD>(dst, e, P.numel[t], slot_vec(P, slot, t), f.x);
+    if (want_sq) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = round_to<DD>(f.x[i]);
+        acc = fmaf(v, v, acc);
+      }
+    }
+  }
+};
+
+template <int DT>
+struct ScaleOp {
+  static constexpr int kRed = 0;
+  float* partials = nullptr;
+  int slot;
+  float s;
+  int mode;
+  struct Frag { float x[4]; };
+  __device__ bool active() const { return true; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
+    store4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  }
+};
+
+template <int DT>
+struct SqnormOp {
+  static constexpr int kRed = 1;
+  float* partials = nullptr;
+  int slot;
+  struct Frag { float x[4]; };
+  __device__ bool active() const { return true; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  }
+  __device__ void apply(const PlanArgs&, int, int64_t, Frag& f, float& acc) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = fmaf(f.x[i], f.x[i], acc);
+  }
+};
+
+template <int DT>
+struct UnscaleOp {
+  static constexpr int kRed = 2;
+  float* partials = nullptr;
+  int slot;
+  const float* inv;  // nullable
+  struct Frag { float x[4]; };
+  __device__ bool active() const { return true; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float& acc) const {
+    const int64_t n = P.numel[t];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (e + i < n && !isfinite(f.x[i])) acc = 1.f;
+    if (inv) {
+      const float s = *inv;
+      if (s != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f.x[i] = f.x[i] * s;
+        store4<DT>(slot_ptr(P, slot, t), e, n, slot_vec(P, slot, t), f.x);
+      }
+    }
+  }
+};
+
+// SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
+template <int GD, int LD>
+struct SgdOp {
+  static constexpr int kRed = 0;
+  float* partials = nullptr;
+  SgdHyper h;
+  const float* gscale;
+  const float* found_inf;
+  struct Frag { float p[4], g[4], b[4]; };
+  __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    const int64_t n = P.numel[t];
+    load4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
+    load4<GD>(slot_ptr(P, 1, t), e, n, slot_vec(P, 1, t), f.g);
+    if (h.mom != 0.f && !h.first) load4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.b);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
+    const int64_t n = P.numel[t];
+    const float gs = gscale ? *gscale : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float g = f.g[i];
+      if (gscale) g = g * gs;                       // clip_grad_norm_ / unscale: grads *= coef
+      if (h.maximize) g = -g;
+      if (h.wd != 0.f) g = fmaf(h.wd, f.p[i], g);   // grad.add(param, alpha=wd)
+      float d = g;
+      if (h.mom != 0.f) {
+        // buf = clone(g) on the first step, else buf.mul_(mom).add_(g, alpha=1-damp)
+        const float b = h.first ? g : fmaf(h.omd, g, f.b[i] * h.mom);
+        f.b[i] = b;
+        d = h.nesterov ? fmaf(h.mom, b, g) : b;     // g.add(buf, alpha=mom)
+      }
+      f.p[i] = fmaf(-h.lr, d, f.p[i]);              // param.add_(d, alpha=-lr)
+    }
+    store4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
+    if (h.mom != 0.f) store4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.b);
+    if constexpr (LD >= 0) store4<LD>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.p);
+  }
+};
+
+// Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
+template <int GD, int LD>
+struct AdamOp {
+  static constexpr int kRed = 0;
+  float* partials = nullptr;
+  AdamHyper h;
+  const float* gscale;
+  const float* found_inf;
+  struct Frag { float p[4], g[4], m[4], v[4]; };
+  __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
+  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
+    const int64_t n = P.numel[t];
+    load4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
+    load4<GD>(slot_ptr(P, 1, t), e, n, slot_vec(P, 1, t), f.g);
+    load4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.m);
+    load4<GS_F32>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.v);
+  }
+  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
+    const int64_t n = P.numel[t];
+    const float gs = gscale ? *gscale : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float g = f.g[i];
+      if (gscale) g = g * gs;
+      if (h.maximize) g = -g;
+      float p = f.p[i];
+      if (h.wd != 0.f) {
+        if (h.adamw) p = p * h.decay;                       // param.mul_(1 - lr*wd)
+        else g = fmaf(h.wd, p, g);                          // grad.add(param, alpha=wd)
+      }
+      const float m = fmaf(h.w1, g - f.m[i], f.m[i]);       // exp_avg.lerp_(g, 1-b1)  (w<0.5)
+      const float v = fmaf(h.w2 * g, g, f.v[i] * h.b2);     // mul_(b2).addcmul_(g, g, 1-b2)
+      const float denom = sqrtf(v) / h.bc2s + h.eps;        // sqrt(v)/bc2_sqrt + eps
+      p = fmaf(h.step_size, m / denom, p);                  // addcdiv_(m, denom, -lr/bc1)
+      f.p[i] = p; f.m[i] = m; f.v[i] = v;
+    }
+    store4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
+    store4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.m);
+    store4<GS_F32>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.v);
+    if constexpr (LD >= 0) store4<LD>(slot_ptr(P, 4, t), e, n, slot_vec(P, 4, t), f.p);
+  }
+};
+
+__global__ void clip_coef_kernel(const float* sq, float max_norm, float eps, float* coef,
+                                 float* norm) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float nrm = sqrtf(sq[0]);
+    if (norm) norm[0] = nrm;
+    const float c = max_norm / (nrm + eps);
+    coef[0] = c < 1.f ? c : 1.f;
+  }
+}
+
+// ------------------------------------------------------------- launching
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      (void)hipSetDevice(dev);
+    } else {
+      prev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <int ILP, class Op>
+int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->n == 0 || p->segs.empty()) {
+    if (Op::kRed != 0 && red_out && !accumulate) HIP_RET(hipMemsetAsync(red_out, 0, 4, s));
+    return GS_OK;
+  }
+  GS_TRY_RET(hip_plan_flush(p, stream));
+  op.partials = p->d_partials;
+  hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(p->grid), dim3(kBlock), 0, s, p->args(), op);
+  HIP_RET(hipGetLastError());
+  if constexpr (Op::kRed != 0) {
+    if (red_out) {
+      hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kBlock), 0, s,
+                         (const float*)p->d_partials, p->grid, red_out, accumulate);
+      HIP_RET(hipGetLastError());
+    }
+  }
+  HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), s));
+  p->last_stream = stream;
+  return GS_OK;
+}
+
+bool flat_aligned(const void* flat) { return (reinterpret_cast<uintptr_t>(flat) & 15u) == 0; }
+
+}  // namespace
+
+// ------------------------------------------------------------- plan memory
+int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int hip_memset_async(void* dst, int value, size_t bytes, void* stream) {
+  HIP_RET(hipMemsetAsync(dst, value, bytes, static_cast<hipStream_t>(stream)));
+  return GS_OK;
+}
+
+int hip_stream_wait(void* waiter, void* signaler) {
+  if (waiter == signaler) return GS_OK;
+  hipEvent_t ev;
+  HIP_RET(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipError_t e1 = hipEventRecord(ev, static_cast<hipStream_t>(signaler));
+  hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(static_cast<hipStream_t>(waiter), ev, 0)
+                                   : e1;
+  (void)hipEventDestroy(ev);  // destruction is deferred until the event completes
+  if (e2 != hipSuccess) return fail(GS_EHIP, std::string("stream wait: ") + hipGetErrorString(e2));
+  return GS_OK;
+}
+
+static size_t table_bytes(const gs_plan* p) {
+  return sizeof(void*) * GS_PLAN_SLOTS * p->n + sizeof(uint32_t) * p->n;
+}
+
+int hip_plan_upload_static(gs_plan* p) {
+  DeviceGuard g(p->device);
+  const size_t sz_segs = sizeof(Seg) * p->segs.size();
+  const size_t sz_tb = sizeof(int32_t) * p->task_begin.size();
+  const size_t sz_n = sizeof(int64_t) * p->n;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t total = al(sz_segs) + al(sz_tb) + al(sz_n) * 2 + 256;
+  HIP_RET(hipMalloc(&p->d_static, total));
+  char* base = static_cast<char*>(p->d_static);
+  std::vector<char> h(total, 0);
+  size_t o = 0;
+  if (sz_segs) std::memcpy(h.data() + o, p->segs.data(), sz_segs);
+  o += al(sz_segs);
+  std::memcpy(h.data() + o, p->task_begin.data(), sz_tb);
+  o += al(sz_tb);
+  if (sz_n) std::memcpy(h.data() + o, p->numel.data(), sz_n);
+  o += al(sz_n);
+  if (sz_n) std::memcpy(h.data() + o, p->off.data(), sz_n);
+  HIP_RET(hipMemcpy(base, h.data(), total, hipMemcpyHostToDevice));
+  const size_t tb = table_bytes(p) + 16;
+  HIP_RET(hipMalloc(&p->d_table, tb));
+  HIP_RET(hipMemset(p->d_table, 0, tb));
+  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * kMaxGrid));
+  HIP_RET(hipHostMalloc(&p->pinned, tb * 4, hipHostMallocDefault));
+  for (int i = 0; i < 4; ++i) {
+    hipEvent_t ev;
+    HIP_RET(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    p->ring_events[i] = ev;
+  }
+  hipEvent_t ev;
+  HIP_RET(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  p->last_event = ev;
+  return GS_OK;
+}
+
+int hip_plan_release(gs_plan* p) {
+  DeviceGuard g(p->device);
+  // make sure nothing in flight still reads the tables
+  if (p->last_event) (void)hipEventSynchronize(static_cast<hipEvent_t>(p->last_event));
+  for (int i = 0; i < 4; ++i) {
+    if (p->ring_events[i]) {
+      (void)hipEventSynchronize(static_cast<hipEvent_t>(p->ring_events[i]));
+      (void)hipEventDestroy(static_cast<hipEvent_t>(p->ring_events[i]));
+    }
+  }
+  if (p->last_event) (void)hipEventDestroy(static_cast<hipEvent_t>(p->last_event));
+  if (p->d_static) (void)hipFree(p->d_static);
+  if (p->d_table) (void)hipFree(p->d_table);
+  if (p->d_partials) (void)hipFree(p->d_partials);
+  if (p->pinned) (void)hipHostFree(p->pinned);
+  return GS_OK;
+}
+
+int hip_plan_flush(gs_plan* p, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // a launch on a new stream is ordered after the plan's previous launch
+  if (p->last_stream != nullptr && p->last_stream != stream)
+    HIP_RET(hipStreamWaitEvent(s, static_cast<hipEvent_t>(p->last_event), 0));
+  if (!p->dirty) return GS_OK;
+  const size_t tb = table_bytes(p);
+  const int k = p->ring;
+  HIP_RET(hipEventSynchronize(static_cast<hipEvent_t>(p->ring_events[k])));
+  char* stage = static_cast<char*>(p->pinned) + k * (tb + 16);
+  std::memcpy(stage, p->h_ptrs.data(), sizeof(void*) * GS_PLAN_SLOTS * p->n);
+  std::memcpy(stage + sizeof(void*) * GS_PLAN_SLOTS * p->n, p->h_align.data(),
+              sizeof(uint32_t) * p->n);
+  HIP_RET(hipMemcpyAsync(p->d_table, stage, tb, hipMemcpyHostToDevice, s));
+  HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->ring_events[k]), s));
+  p->ring = (k + 1) & 3;
+  p->dirty = false;
+  return GS_OK;
+}
+
+// ------------------------------------------------------------- dispatchers
+#define GS_DISPATCH_FLOAT(DT, NAME, ...)                        \
+  switch (DT) {                                                 \
+    case GS_F32: { constexpr int NAME = GS_F32; __VA_ARGS__; break; }   \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; } \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }   \
+    default: return fail(GS_EINVAL, "unsupported floating dtype");      \
+  }
+
+#define GS_DISPATCH_LOWP(DT, NAME, ...)                                  \
+  switch (DT) {                                                          \
+    case -1: { constexpr int NAME = -1; __VA_ARGS__; break; }            \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; }  \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }    \
+    default: return fail(GS_EINVAL, "unsupported low-precision dtype");  \
+  }
+
+int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
+             void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(src_dt, SD, GS_DISPATCH_FLOAT(flat_dt, FD, {
+    PackOp<SD, FD> op;
+    op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s; op.mode = mode;
+    return launch<4>(p, op, stream);
+  }));
+  return GS_OK;
+}
+
+int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
+               int acc, void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
+    UnpackOp<FD, DD> op;
+    op.want_sq = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
+    return launch<4>(p, op, stream, sq, acc);
+  }));
+  return GS_OK;
+}
+
+int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(dt, DT, {
+    ScaleOp<DT> op;
+    op.slot = slot; op.s = s; op.mode = mode;
+    return launch<4>(p, op, stream);
+  });
+  return GS_OK;
+}
+
+int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(dt, DT, {
+    SqnormOp<DT> op;
+    op.slot = slot;
+    return launch<4>(p, op, stream, sq, acc);
+  });
+  return GS_OK;
+}
+
+int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm,
+                  void* stream) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     sq, max_norm, eps, coef, norm);
+  HIP_RET(hipGetLastError());
+  return GS_OK;
+}
+
+int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
+                      void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(dt, DT, {
+    UnscaleOp<DT> op;
+    op.slot = slot; op.inv = inv;
+    // found_inf accumulates (max) into the caller's flag, as torch's kernel does
+    return launch<4>(p, op, stream, found, 1);
+  });
+  return GS_OK;
+}
+
+int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
+            void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
+    SgdOp<GD, LD> op;
+    op.h = h; op.gscale = gsc; op.found_inf = fi;
+    return launch<2>(p, op, stream);
+  }));
+  return GS_OK;
+}
+
+int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
+             void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
+    AdamOp<GD, LD> op;
+    op.h = h; op.gscale = gsc; op.found_inf = fi;
+    return launch<2>(p, op, stream);
+  }));
+  return GS_OK;
+}
+
+}  // namespace gs

@@ -1,0 +1,298 @@
+// libgsync: error plumbing, multi-tensor plans and the plan-op entry points,
+// plus the bucket-assignment restatement of torch's Reducer.
+#include <algorithm>
+#include <map>
+#include <new>
+
+#include "gs_common.h"
+
+namespace gs {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+}  // namespace gs
+
+using namespace gs;
+
+gs::PlanArgs gs_plan::args() const {
+  PlanArgs a{};
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char* base = static_cast<char*>(d_static);
+  size_t o = 0;
+  a.segs = reinterpret_cast<const Seg*>(base + o);
+  o += al(sizeof(Seg) * segs.size());
+  a.task_begin = reinterpret_cast<const int32_t*>(base + o);
+  o += al(sizeof(int32_t) * task_begin.size());
+  a.numel = reinterpret_cast<const int64_t*>(base + o);
+  o += al(sizeof(int64_t) * n);
+  a.off = reinterpret_cast<const int64_t*>(base + o);
+  a.ptrs = static_cast<void* const*>(d_table);
+  a.align = reinterpret_cast<const uint32_t*>(static_cast<char*>(d_table) +
+                                              sizeof(void*) * GS_PLAN_SLOTS * n);
+  a.n = n;
+  a.n_tasks = static_cast<int32_t>(task_begin.size()) - 1;
+  return a;
+}
+
+extern "C" {
+
+int gs_version(void) { return GSYNC_VERSION; }
+const char* gs_last_error(void) { return gs::g_last_error.c_str(); }
+int gs_device_count(void) { return hip_device_count(); }
+
+int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* numels,
+                   int64_t align_elems, gs_plan** out) {
+  GS_CHECK_ARG(out != nullptr, "gs_plan_create: out is NULL");
+  GS_CHECK_ARG(n_tensors >= 0, "gs_plan_create: n_tensors < 0");
+  GS_CHECK_ARG(n_tensors == 0 || numels != nullptr, "gs_plan_create: numels is NULL");
+  GS_CHECK_ARG(device_kind == GS_DEV_HOST || device_kind == GS_DEV_HIP,
+               "gs_plan_create: bad device_kind");
+  GS_CHECK_ARG(align_elems >= 0 && (align_elems == 0 || align_elems % kUnit == 0),
+               "gs_plan_create: align_elems must be 0 or a multiple of 4");
+  if (device_kind == GS_DEV_HIP && hip_device_count() <= device)
+    return fail(GS_ENODEV, "gs_plan_create: HIP device " + std::to_string(device) +
+                               " not available");
+  gs_plan* p = new (std::nothrow) gs_plan();
+  if (!p) return fail(GS_ENOMEM, "gs_plan_create: out of host memory");
+  p->kind = device_kind;
+  p->device = device;
+  p->n = n_tensors;
+  p->align_elems = align_elems;
+  p->numel.assign(numels, numels + n_tensors);
+  p->off.resize(n_tensors);
+  int64_t cur = 0;
+  auto rup = [&](int64_t x) { return align_elems ? (x + align_elems - 1) / align_elems * align_elems : x; };
+  for (int t = 0; t < n_tensors; ++t) {
+    if (numels[t] < 0) {
+      delete p;
+      return fail(GS_EINVAL, "gs_plan_create: negative numel");
+    }
+    cur = rup(cur);
+    p->off[t] = cur;
+    cur += numels[t];
+  }
+  p->flat_numel = rup(cur);
+  // segments and tasks
+  for (int t = 0; t < n_tensors; ++t) {
+    const int64_t units = (numels[t] + kUnit - 1) / kUnit;
+    for (int64_t u = 0; u < units; u += kSegUnits) {
+      Seg s{};
+      s.unit_begin = u;
+      s.tensor = t;
+      s.units = static_cast<int32_t>(std::min<int64_t>(kSegUnits, units - u));
+      p->segs.push_back(s);
+    }
+  }
+  p->task_begin.push_back(0);
+  int32_t tu = 0, tc = 0;
+  for (size_t i = 0; i < p->segs.size(); ++i) {
+    Seg& s = p->segs[i];
+    if (tc > 0 && (tu + s.units > kTaskUnits || tc == kMaxSegPerTask)) {
+      p->task_begin.push_back(static_cast<int32_t>(i));
+      tu = 0;
+      tc = 0;
+    }
+    s.task_off = tu;
+    tu += s.units;
+    ++tc;
+  }
+  if (!p->segs.empty()) p->task_begin.push_back(static_cast<int32_t>(p->segs.size()));
+  const int n_tasks = static_cast<int>(p->task_begin.size()) - 1;
+  p->grid = std::max(1, std::min(n_tasks, kMaxGrid));
+  p->h_ptrs.assign(static_cast<size_t>(GS_PLAN_SLOTS) * n_tensors, nullptr);
+  p->h_align.assign(n_tensors, 0u);
+  if (device_kind == GS_DEV_HIP) {
+    int rc = hip_plan_upload_static(p);
+    if (rc != GS_OK) {
+      hip_plan_release(p);
+      delete p;
+      return rc;
+    }
+  }
+  *out = p;
+  return GS_OK;
+}
+
+int gs_plan_destroy(gs_plan* p) {
+  if (!p) return GS_OK;
+  if (p->kind == GS_DEV_HIP) hip_plan_release(p);
+  delete p;
+  return GS_OK;
+}
+
+int64_t gs_plan_flat_numel(gs_plan* p) { return p ? p->flat_numel : -1; }
+
+int gs_plan_offsets(gs_plan* p, int64_t* out) {
+  GS_CHECK_ARG(p && out, "gs_plan_offsets: NULL argument");
+  std::copy(p->off.begin(), p->off.end(), out);
+  return GS_OK;
+}
+
+int gs_plan_n_tasks(gs_plan* p) { return p ? static_cast<int>(p->task_begin.size()) - 1 : -1; }
+
+int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* /*stream*/) {
+  GS_CHECK_ARG(p != nullptr, "gs_plan_set_ptrs: NULL plan");
+  GS_CHECK_ARG(slot >= 0 && slot < GS_PLAN_SLOTS, "gs_plan_set_ptrs: slot out of range");
+  GS_CHECK_ARG(p->n == 0 || ptrs != nullptr, "gs_plan_set_ptrs: NULL ptrs");
+  void** row = p->h_ptrs.data() + static_cast<size_t>(slot) * p->n;
+  for (int t = 0; t < p->n; ++t) {
+    if (row[t] != ptrs[t]) {
+      row[t] = ptrs[t];
+      const uint32_t bit = 1u << slot;
+      const bool al = (reinterpret_cast<uintptr_t>(ptrs[t]) & 15u) == 0;
+      p->h_align[t] = al ? (p->h_align[t] | bit) : (p->h_align[t] & ~bit);
+      p->dirty = true;
+    }
+  }
+  return GS_OK;
+}
+
+#define PLAN_OK(p) GS_CHECK_ARG((p) != nullptr, "NULL plan")
+#define SLOT_OK(s) GS_CHECK_ARG((s) >= 0 && (s) < GS_PLAN_SLOTS, "slot out of range")
+
+int gs_pack(gs_plan* p, int src_slot, int src_dtype, void* flat, int flat_dtype, float scale,
+            int scale_mode, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(src_slot);
+  GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_pack: NULL flat buffer");
+  GS_CHECK_ARG(scale_mode >= GS_SCALE_NONE && scale_mode <= GS_SCALE_DIV, "gs_pack: bad scale_mode");
+  if (p->kind == GS_DEV_HOST) return host_pack(p, src_slot, src_dtype, flat, flat_dtype, scale, scale_mode);
+  return hip_pack(p, src_slot, src_dtype, flat, flat_dtype, scale, scale_mode, stream);
+}
+
+int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
+              float* sqnorm_dev, int accumulate, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(dst_slot);
+  GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_unpack: NULL flat buffer");
+  if (p->kind == GS_DEV_HOST)
+    return host_unpack(p, flat, flat_dtype, dst_slot, dst_dtype, sqnorm_dev, accumulate);
+  return hip_unpack(p, flat, flat_dtype, dst_slot, dst_dtype, sqnorm_dev, accumulate, stream);
+}
+
+int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(scale_mode == GS_SCALE_MUL || scale_mode == GS_SCALE_DIV, "gs_scale: bad scale_mode");
+  if (p->kind == GS_DEV_HOST) return host_scale(p, slot, dtype, s, scale_mode);
+  return hip_scale(p, slot, dtype, s, scale_mode, stream);
+}
+
+int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(sqnorm_dev != nullptr, "gs_sqnorm: NULL output");
+  if (p->kind == GS_DEV_HOST) return host_sqnorm(p, slot, dtype, sqnorm_dev, accumulate);
+  return hip_sqnorm(p, slot, dtype, sqnorm_dev, accumulate, stream);
+}
+
+int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,
+                 float* coef_dev, float* norm_dev, void* stream) {
+  GS_CHECK_ARG(sqnorm_dev && coef_dev, "gs_clip_coef: NULL argument");
+  if (device_kind == GS_DEV_HOST)
+    return host_clip_coef(sqnorm_dev, max_norm, eps, coef_dev, norm_dev);
+  return hip_clip_coef(sqnorm_dev, max_norm, eps, coef_dev, norm_dev, stream);
+}
+
+int gs_unscale_check(gs_plan* p, int slot, int dtype, const float* inv_scale_dev,
+                     float* found_inf_dev, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(found_inf_dev != nullptr, "gs_unscale_check: NULL found_inf");
+  if (p->kind == GS_DEV_HOST) return host_unscale_check(p, slot, dtype, inv_scale_dev, found_inf_dev);
+  return hip_unscale_check(p, slot, dtype, inv_scale_dev, found_inf_dev, stream);
+}
+
+int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double momentum,
+                double dampening, double weight_decay, int nesterov, int maximize, int first_step,
+                const float* grad_scale_dev, const float* found_inf_dev, void* stream) {
+  PLAN_OK(p);
+  GS_CHECK_ARG(!nesterov || (momentum > 0 && dampening == 0),
+               "Nesterov momentum requires a momentum and zero dampening");
+  const SgdHyper h = make_sgd(lr, momentum, dampening, weight_decay, nesterov, maximize, first_step);
+  if (p->kind == GS_DEV_HOST) return host_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
+  return hip_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
+}
+
+int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double beta1,
+                 double beta2, double eps, double weight_decay, int adamw, int maximize,
+                 double step_size, double bias_correction2_sqrt, const float* grad_scale_dev,
+                 const float* found_inf_dev, void* stream) {
+  PLAN_OK(p);
+  GS_CHECK_ARG(bias_correction2_sqrt > 0, "gs_adam_step: bias_correction2_sqrt must be > 0");
+  const AdamHyper h = make_adam(lr, beta1, beta2, eps, weight_decay, adamw, maximize, step_size,
+                                bias_correction2_sqrt);
+  if (p->kind == GS_DEV_HOST) return host_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
+  return hip_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
+}
+
+int gs_stream_wait(void* waiter, void* signaler) { return hip_stream_wait(waiter, signaler); }
+
+// Restatement of compute_bucket_assignment_by_size (torch c10d reducer.cpp,
+// declared at T:include/torch/csrc/distributed/c10d/reducer.hpp:590-595):
+// per (dtype, device) key a bucket accumulates tensors until its byte size
+// reaches the current limit (>=, so a bucket may exceed it); each key then
+// advances to the next limit.  Leftover buckets are appended; without an
+// explicit order the result is sorted by the smallest tensor index.
+int gs_compute_bucket_assignment(int n, const int64_t* nbytes, const int32_t* dtype_keys,
+                                 const int32_t* order, int n_limits, const int64_t* limits,
+                                 int32_t* bucket_of, int32_t* bucket_members,
+                                 int32_t* bucket_counts) {
+  GS_CHECK_ARG(n >= 0 && nbytes && n_limits > 0 && limits, "gs_compute_bucket_assignment: bad args");
+  struct Acc {
+    std::vector<int32_t> idx;
+    int64_t size = 0;
+    int lim = 0;
+  };
+  std::map<int32_t, Acc> acc;  // key -> open bucket
+  std::vector<int32_t> key_order;
+  std::vector<std::vector<int32_t>> result;
+  for (int i = 0; i < n; ++i) {
+    const int32_t t = order ? order[i] : i;
+    GS_CHECK_ARG(t >= 0 && t < n, "gs_compute_bucket_assignment: order out of range");
+    const int32_t key = dtype_keys ? dtype_keys[t] : 0;
+    auto it = acc.find(key);
+    if (it == acc.end()) {
+      it = acc.emplace(key, Acc{}).first;
+      key_order.push_back(key);
+    }
+    Acc& b = it->second;
+    b.idx.push_back(t);
+    b.size += nbytes[t];
+    if (b.size >= limits[b.lim]) {
+      result.push_back(std::move(b.idx));
+      b.idx.clear();
+      b.size = 0;
+      if (b.lim + 1 < n_limits) ++b.lim;
+    }
+  }
+  for (int32_t key : key_order) {
+    Acc& b = acc[key];
+    if (!b.idx.empty()) result.push_back(std::move(b.idx));
+  }
+  if (!order) {
+    std::stable_sort(result.begin(), result.end(),
+                     [](const std::vector<int32_t>& a, const std::vector<int32_t>& b) {
+                       return *std::min_element(a.begin(), a.end()) <
+                              *std::min_element(b.begin(), b.end());
+                     });
+  }
+  int pos = 0;
+  for (size_t bi = 0; bi < result.size(); ++bi) {
+    if (bucket_counts) bucket_counts[bi] = static_cast<int32_t>(result[bi].size());
+    for (int32_t t : result[bi]) {
+      if (bucket_of) bucket_of[t] = static_cast<int32_t>(bi);
+      if (bucket_members) bucket_members[pos] = t;
+      ++pos;
+    }
+  }
+  return static_cast<int>(result.size());
+}
+
+}  // extern "C"

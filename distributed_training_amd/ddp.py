@@ -1,0 +1,584 @@
+"""Drop-in ``DistributedDataParallel`` on the libgsync gradient-sync engine.
+
+Same constructor, attribute and call surface as torch's
+``torch.nn.parallel.DistributedDataParallel`` (T:nn/parallel/distributed.py:653-953)
+as the reference scripts use it (``DDP(model)`` at
+R:resnet/pytorch_ddp/ddp_train.py:95; colossal ``TorchDDPPlugin`` at
+R:resnet/colossal/colossal_train.py:131-132,159): ``.module``, ``forward``,
+``no_sync()``, ``register_comm_hook``, ``state_dict`` with the ``module.``
+prefix, ``_get_ddp_logging_data()``.
+
+What changes is underneath:
+
+* the c10d Reducer is replaced by the libgsync bucketer (C++), driven by one
+  ``register_post_accumulate_grad_hook`` per parameter;
+* a bucket is packed (fused 1/world_size scale + cast) by one gfx950
+  multi-tensor kernel when its last gradient arrives, all-reduced by RCCL on
+  libgsync's own stream and unpacked there, overlapped with the rest of
+  backward (torch: one ATen launch per parameter for pack and for unpack);
+* BN buffers are broadcast from rank 0 before every forward through the same
+  pack kernel + one RCCL broadcast (T:nn/parallel/distributed.py:2178-2221).
+
+Bucketing semantics follow torch: first iteration one bucket (sys.maxsize,
+:1199-1200), then buckets rebuilt once in gradient-ready order with a
+1 MiB first bucket and ``bucket_cap_mb`` (25 MiB) caps, rank 0's layout
+broadcast to all ranks (Reducer::rebuild_buckets / sync_bucket_indices).
+
+On CPU tensors (the CPU/gloo configuration) the same bucketer runs its host
+backend and the collective is torch's gloo all-reduce.
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+from contextlib import contextmanager
+from typing import Any, Callable
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import _lib as L
+from .comm import get_communicator
+from .multi_tensor import TensorListPlan, dense_like_param, is_dense
+
+DEFAULT_FIRST_BUCKET_BYTES = getattr(dist, "_DEFAULT_FIRST_BUCKET_BYTES", 1024 * 1024)
+BUCKET_ALIGN_ELEMS = 64  # 256 B (fp32) per-parameter alignment inside a bucket
+
+
+def compute_bucket_assignment_by_size(tensors, size_limits, order=None):
+    """Restatement of dist._compute_bucket_assignment_by_size (libgsync C++).
+
+    Returns a list of buckets, each a list of tensor indices.  ``order``
+    (gradient-ready order) disables the final sort, as Reducer::rebuild_buckets.
+    """
+    n = len(tensors)
+    nbytes = L.i64_array([t.numel() * t.element_size() for t in tensors])
+    keys = []
+    key_ids: dict = {}
+    for t in tensors:
+        k = (t.dtype, t.device)
+        keys.append(key_ids.setdefault(k, len(key_ids)))
+    limits = [int(min(x, 2**62)) for x in size_limits]
+    bucket_of = (ctypes.c_int32 * max(1, n))()
+    members = (ctypes.c_int32 * max(1, n))()
+    counts = (ctypes.c_int32 * max(1, n))()
+    nb = L.check(
+        L.lib().gs_compute_bucket_assignment(
+            n, nbytes, L.i32_array(keys), None if order is None else L.i32_array(order), len(limits),
+            L.i64_array(limits), bucket_of, members, counts),
+        "gs_compute_bucket_assignment",
+    )
+    out, pos = [], 0
+    for b in range(nb):
+        out.append([int(members[pos + k]) for k in range(counts[b])])
+        pos += counts[b]
+    return out
+
+
+class GradBucket:
+    """Mirror of torch.distributed.GradBucket (T:include/torch/csrc/distributed/c10d/comm.hpp:20-98)."""
+
+    def __init__(self, index, buffer, params, offsets, is_last):
+        self._index = index
+        self._buffer = buffer
+        self._params = params
+        self._offsets = offsets
+        self._is_last = is_last
+
+    def index(self):
+        return self._index
+
+    def buffer(self):
+        return self._buffer
+
+    def set_buffer(self, t):
+        self._buffer.copy_(t)
+
+    def parameters(self):
+        return list(self._params)
+
+    def gradients(self):
+        buf = self._buffer
+        return [
+            buf.as_strided(p.size(), p.stride(), buf.storage_offset() + off)
+            for p, off in zip(self._params, self._offsets)
+        ]
+
+    def is_last(self):
+        return self._is_last
+
+
+class _Bucketer:
+    """Python owner of one gs_bucketer + its torch-allocated bucket storage."""
+
+    def __init__(self, ddp, buckets, flags):
+        self.ddp = ddp
+        params = ddp._params
+        self.buckets = buckets
+        self.flags = flags
+        kind = L.GS_DEV_HIP if ddp.device.type == "cuda" else L.GS_DEV_HOST
+        counts = [len(b) for b in buckets]
+        members = [i for b in buckets for i in b]
+        h = ctypes.c_void_p()
+        comm = ddp._comm.handle if (ddp._comm is not None) else None
+        L.check(
+            L.lib().gs_bucketer_create(
+                comm, kind, ddp._dev_index, len(params), L.i64_array([p.numel() for p in params]),
+                L.gs_dtype(ddp._grad_dtype), len(buckets), L.i32_array(counts), L.i32_array(members),
+                L.gs_dtype(ddp._bucket_dtype), BUCKET_ALIGN_ELEMS, float(ddp.world_size), flags, ctypes.byref(h)),
+            "gs_bucketer_create",
+        )
+        self.handle = h
+        self.buffers = []
+        for b in range(len(buckets)):
+            n = ctypes.c_int64()
+            L.check(L.lib().gs_bucketer_bucket_numel(h, b, ctypes.byref(n)), "gs_bucketer_bucket_numel")
+            buf = torch.zeros(n.value, dtype=ddp._bucket_dtype, device=ddp.device)
+            L.check(L.lib().gs_bucketer_set_bucket_buffer(h, b, buf.data_ptr()), "gs_bucketer_set_bucket_buffer")
+            self.buffers.append(buf)
+        self.loc = []
+        for i in range(len(params)):
+            bi, off = ctypes.c_int32(), ctypes.c_int64()
+            L.check(L.lib().gs_bucketer_param_location(h, i, ctypes.byref(bi), ctypes.byref(off)),
+                    "gs_bucketer_param_location")
+            self.loc.append((bi.value, off.value))
+        self.offsets_in_bucket = [[self.loc[i][1] for i in b] for b in buckets]
+        self._ready = (ctypes.c_int32 * max(1, len(buckets)))()
+        self._n_ready = ctypes.c_int32()
+
+    def bucket_view(self, i):
+        b, off = self.loc[i]
+        p = self.ddp._params[i]
+        buf = self.buffers[b]
+        return buf.as_strided(p.size(), p.stride(), off)
+
+    def logical_bytes(self):
+        params = self.ddp._params
+        return [sum(params[i].numel() for i in b) * torch.tensor([], dtype=self.ddp._bucket_dtype).element_size()
+                for b in self.buckets]
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            L.lib().gs_bucketer_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module, device_ids=None, output_device=None, dim=0, broadcast_buffers=True,
+                 init_sync=True, process_group=None, bucket_cap_mb=None, find_unused_parameters=False,
+                 check_reduction=False, gradient_as_bucket_view=False, static_graph=False,
+                 delay_all_reduce_named_params=None, param_to_hook_all_reduce=None, mixed_precision=None,
+                 device_mesh=None, skip_all_reduce_unused_params=False, *, bucket_dtype=None,
+                 collective: str = "auto"):
+        super().__init__()
+        if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
+            raise NotImplementedError("delay_all_reduce_named_params is outside the gradient-sync path")
+        if mixed_precision is not None or device_mesh is not None:
+            raise NotImplementedError("DDP mixed_precision / device_mesh are outside the gradient-sync path")
+        if not dist.is_initialized():
+            raise RuntimeError("Default process group has not been initialized, please make sure to call "
+                               "init_process_group.")
+        self.module = module
+        self.process_group = process_group if process_group is not None else dist.group.WORLD
+        self.world_size = dist.get_world_size(self.process_group)
+        self.rank = dist.get_rank(self.process_group)
+        self.dim = dim
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.gradient_as_bucket_view = gradient_as_bucket_view
+        self.static_graph = static_graph
+        self.require_backward_grad_sync = True
+        self.require_forward_param_sync = True
+        self.bucket_bytes_cap_default = bucket_cap_mb is None
+        self.bucket_bytes_cap = int((25 if bucket_cap_mb is None else bucket_cap_mb) * 1024 * 1024)
+        self.first_bucket_bytes_cap = DEFAULT_FIRST_BUCKET_BYTES if self.bucket_bytes_cap_default else self.bucket_bytes_cap
+
+        # parameters handed to the bucketer: module order, requires_grad, no duplicates
+        seen = set()
+        self._params, self._param_names = [], []
+        for name, p in module.named_parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self._params.append(p)
+                self._param_names.append(name)
+        if not self._params:
+            raise RuntimeError("DistributedDataParallel is not needed when a module doesn't have any "
+                               "parameter that requires a gradient.")
+        devices = {p.device for p in self._params}
+        if len(devices) != 1:
+            raise ValueError(f"DDP module parameters must live on one device, found {devices}")
+        self.device = next(iter(devices))
+        self.device_type = self.device.type
+        self.device_ids = device_ids if device_ids is None else [torch.device(d).index if not isinstance(d, int) else d for d in device_ids]
+        self.output_device = output_device
+        dtypes = {p.dtype for p in self._params}
+        if len(dtypes) != 1:
+            raise NotImplementedError(f"parameters of several dtypes are not supported yet: {dtypes}")
+        self._grad_dtype = next(iter(dtypes))
+        self._bucket_dtype = bucket_dtype if bucket_dtype is not None else self._grad_dtype
+        if self.device.type == "cuda":
+            self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            if not L.available():
+                raise L.GsyncUnavailable(L._load_error)
+        else:
+            self._dev_index = 0
+        self._backend = dist.get_backend(self.process_group)
+
+        # library-owned RCCL communicator for CUDA tensors over an nccl (=RCCL) group
+        self._comm = None
+        if self.device.type == "cuda" and collective != "process_group" and self._backend == "nccl":
+            self._comm = get_communicator(None if self.process_group is dist.group.WORLD else self.process_group,
+                                          torch.device("cuda", self._dev_index))
+        self._comm_hook: tuple[Any, Callable] | None = None
+        self._buffers_plan = None
+        self._sqnorm_target: torch.Tensor | None = None
+
+        if init_sync:
+            self._verify_param_shape_across_processes()
+            self._sync_module_states()
+
+        if static_graph or not find_unused_parameters:
+            limits = [sys.maxsize]
+        elif self.bucket_bytes_cap_default:
+            limits = [DEFAULT_FIRST_BUCKET_BYTES, self.bucket_bytes_cap]
+        else:
+            limits = [self.bucket_bytes_cap]
+        buckets = compute_bucket_assignment_by_size(self._params, limits)
+        # "reverse list of buckets because we want to approximate the order in
+        # which their gradients are produced" (T:nn/parallel/distributed.py:1222)
+        self._bucketer = self._make_bucketer(list(reversed(buckets)))
+        self._has_rebuilt_buckets = False
+        self._ready_order: list[int] = []
+        self._in_backward = False
+        self._finalize_queued = False
+        self._stream = None
+        self._pending: dict[int, Any] = {}
+        self._num_iterations = 0
+        self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                              for i, p in enumerate(self._params)]
+
+    # ------------------------------------------------------------------ setup
+    def _flags(self):
+        flags = 0
+        if self._comm is not None and self._comm_hook is None:
+            flags |= L.GS_BKT_AUTO_COLLECTIVE
+        if self.gradient_as_bucket_view:
+            flags |= L.GS_BKT_GRAD_VIEW
+        if self._comm_hook is not None:
+            flags |= L.GS_BKT_NO_SCALE
+        return flags
+
+    def _make_bucketer(self, buckets):
+        old = getattr(self, "_bucketer", None)
+        if old is not None:
+            old.close()
+        return _Bucketer(self, buckets, self._flags())
+
+    def _verify_param_shape_across_processes(self):
+        if self.world_size == 1:
+            return
+        dev = self.device if self._backend == "nccl" else torch.device("cpu")
+        meta = torch.tensor([len(self._params), sum(p.numel() for p in self._params),
+                             hash(tuple(tuple(p.shape) for p in self._params)) % (2**61)],
+                            dtype=torch.int64, device=dev)
+        lo, hi = meta.clone(), meta.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.process_group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.process_group)
+        if not torch.equal(lo, hi):
+            raise RuntimeError("DDP expects same model across all ranks, but the parameter shapes differ "
+                               f"(rank {self.rank}: {meta.tolist()})")
+
+    def _module_buffers(self):
+        return [b for b in self.module.buffers()]
+
+    def _broadcast_tensors(self, tensors):
+        """Broadcast tensors from rank 0: floating tensors go through the
+        libgsync pack kernel + one broadcast + unpack; others through a cat."""
+        if self.world_size == 1 or not tensors:
+            return
+        floats = [t for t in tensors if t.is_floating_point() and is_dense(t)]
+        others = [t for t in tensors if not (t.is_floating_point() and is_dense(t))]
+        by_dtype: dict = {}
+        for t in floats:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for dt, ts in by_dtype.items():
+            plan = TensorListPlan([t.numel() for t in ts], self.device, align=BUCKET_ALIGN_ELEMS)
+            plan.set_ptrs(0, ts)
+            flat = torch.zeros(plan.flat_numel, dtype=dt, device=self.device)
+            if self.rank == 0:
+                plan.pack(0, dt, flat)
+            self._bcast_flat(flat)
+            if self.rank != 0:
+                plan.unpack(flat, 0, dt)
+        if others:
+            flat = torch.cat([t.reshape(-1) for t in others])
+            self._bcast_flat(flat)
+            if self.rank != 0:
+                off = 0
+                for t in others:
+                    t.copy_(flat[off:off + t.numel()].view_as(t))
+                    off += t.numel()
+
+    def _bcast_flat(self, flat):
+        if self._comm is not None:
+            self._comm.broadcast(flat, root=0, stream=L.stream_ptr(self.device))
+        else:
+            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, 0)
+                           if self.process_group is not dist.group.WORLD else 0, group=self.process_group)
+
+    @torch.no_grad()
+    def _sync_module_states(self):
+        """_sync_module_states: params + buffers from rank 0 (T:nn/parallel/distributed.py:860-870)."""
+        self._broadcast_tensors([p.detach() for p in self._params] + self._module_buffers())
+
+    @torch.no_grad()
+    def _sync_buffers(self):
+        """Per-forward BN buffer broadcast (T:nn/parallel/distributed.py:2178-2221),
+        pack kernel + one collective + unpack, plan cached across steps."""
+        bufs = self._module_buffers()
+        if self.world_size == 1 or not bufs:
+            return
+        floats = [t for t in bufs if t.is_floating_point() and is_dense(t)]
+        others = [t for t in bufs if not (t.is_floating_point() and is_dense(t))]
+        key = tuple(id(t) for t in bufs)
+        if self._buffers_plan is None or self._buffers_plan[0] != key:
+            plans = []
+            by_dtype: dict = {}
+            for t in floats:
+                by_dtype.setdefault(t.dtype, []).append(t)
+            for dt, ts in by_dtype.items():
+                plan = TensorListPlan([t.numel() for t in ts], self.device, align=BUCKET_ALIGN_ELEMS)
+                flat = torch.zeros(plan.flat_numel, dtype=dt, device=self.device)
+                plans.append((plan, ts, dt, flat))
+            self._buffers_plan = (key, plans)
+        for plan, ts, dt, flat in self._buffers_plan[1]:
+            plan.set_ptrs(0, ts)
+            if self.rank == 0:
+                plan.pack(0, dt, flat)
+            self._bcast_flat(flat)
+            if self.rank != 0:
+                plan.unpack(flat, 0, dt)
+        if others:
+            flat = torch.cat([t.reshape(-1) for t in others])
+            self._bcast_flat(flat)
+            if self.rank != 0:
+                off = 0
+                for t in others:
+                    t.copy_(flat[off:off + t.numel()].view_as(t))
+                    off += t.numel()
+
+    # ------------------------------------------------------------------ forward
+    def _will_sync_module_buffers(self):
+        return self.require_forward_param_sync and self.broadcast_buffers and len(self._module_buffers()) != 0
+
+    def forward(self, *inputs, **kwargs):
+        grad_sync = torch.is_grad_enabled() and self.require_backward_grad_sync
+        if grad_sync:
+            self._maybe_rebuild_buckets()
+        if self._will_sync_module_buffers():
+            self._sync_buffers()
+        if self.device_ids:
+            dev = torch.device(self.device_type, self.device_ids[0])
+            inputs = tuple(x.to(dev, non_blocking=True) if isinstance(x, torch.Tensor) else x for x in inputs)
+            kwargs = {k: (v.to(dev, non_blocking=True) if isinstance(v, torch.Tensor) else v) for k, v in kwargs.items()}
+        output = self.module(*inputs, **kwargs)
+        if grad_sync:
+            self.require_forward_param_sync = True
+            self._prepare_for_backward()
+        else:
+            self.require_forward_param_sync = False
+        return output
+
+    def _prepare_for_backward(self):
+        if self._in_backward and self._finalize_queued:
+            raise RuntimeError(
+                "Expected to have finished reduction in the prior iteration before starting a new one. "
+                "This error indicates that your module has parameters that were not used in producing loss.")
+        sq = self._sqnorm_target
+        L.check(L.lib().gs_bucketer_prepare(self._bucketer.handle, None if sq is None else sq.data_ptr()),
+                "gs_bucketer_prepare")
+        self._in_backward = True
+        self._finalize_queued = False
+        self._pending = {}
+        self._record_order = not self._has_rebuilt_buckets and (self.static_graph or not self.find_unused_parameters)
+        if self._record_order:
+            self._ready_order = []
+
+    @contextmanager
+    def no_sync(self):
+        """Gradients accumulate locally; synchronised on the first backward after exit."""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    # ------------------------------------------------------------------ hooks
+    def _make_hook(self, idx):
+        def hook(param):
+            if not self._in_backward:
+                return
+            if not self._finalize_queued:
+                self._finalize_queued = True
+                self._stream = L.stream_ptr(self.device)
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+            if self._record_order:
+                self._ready_order.append(idx)
+            g = param.grad
+            if not dense_like_param(g, param):
+                dense = torch.empty_like(param)
+                dense.copy_(g)
+                param.grad = g = dense
+            b = self._bucketer
+            L.check(L.lib().gs_bucketer_mark_ready(b.handle, idx, g.data_ptr(), self._stream, b._ready,
+                                                   ctypes.byref(b._n_ready)), "gs_bucketer_mark_ready")
+            if b._n_ready.value and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+                self._launch_external([b._ready[k] for k in range(b._n_ready.value)])
+
+        return hook
+
+    def _launch_external(self, bucket_ids):
+        b = self._bucketer
+        nb = len(b.buckets)
+        for bi in bucket_ids:
+            buf = b.buffers[bi]
+            if self._comm_hook is not None:
+                state, hook = self._comm_hook
+                gb = GradBucket(bi, buf, [self._params[i] for i in b.buckets[bi]], b.offsets_in_bucket[bi],
+                                bi == nb - 1)
+                self._pending[bi] = ("fut", hook(state, gb))
+            elif self._comm is not None:
+                self._comm.all_reduce(buf, stream=L.stream_ptr(self.device))
+                self._pending[bi] = ("done", None)
+            else:
+                self._pending[bi] = ("work", dist.all_reduce(buf, group=self.process_group, async_op=True))
+
+    def _finalize_backward(self):
+        b = self._bucketer
+        if self.find_unused_parameters:
+            L.check(L.lib().gs_bucketer_mark_unused(b.handle, self._stream, b._ready, ctypes.byref(b._n_ready)),
+                    "gs_bucketer_mark_unused")
+            if b._n_ready.value and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+                self._launch_external([b._ready[k] for k in range(b._n_ready.value)])
+        for bi in sorted(self._pending):
+            kind, obj = self._pending[bi]
+            if kind == "work":
+                obj.wait()
+            elif kind == "fut":
+                res = obj.wait()
+                if isinstance(res, (list, tuple)):
+                    res = res[0]
+                if res is not None and res.data_ptr() != b.buffers[bi].data_ptr():
+                    b.buffers[bi].copy_(res.reshape(-1)[: b.buffers[bi].numel()])
+        self._pending = {}
+        L.check(L.lib().gs_bucketer_finalize(b.handle, self._stream), "gs_bucketer_finalize")
+        if self.gradient_as_bucket_view:
+            for i, p in enumerate(self._params):
+                if p.grad is not None:
+                    view = b.bucket_view(i)
+                    if p.grad.data_ptr() != view.data_ptr():
+                        p.grad = view
+        self._in_backward = False
+        self._finalize_queued = False
+        self._num_iterations += 1
+
+    def _maybe_rebuild_buckets(self):
+        if self._has_rebuilt_buckets or not (self.static_graph or not self.find_unused_parameters):
+            return
+        if len(self._ready_order) != len(self._params) or self._num_iterations == 0:
+            return
+        limits = [self.first_bucket_bytes_cap, self.bucket_bytes_cap]
+        buckets = compute_bucket_assignment_by_size(self._params, limits, order=self._ready_order)
+        buckets = self._sync_bucket_indices(buckets)
+        if self.gradient_as_bucket_view:
+            for p in self._params:  # grads must not alias the old buckets once they are freed
+                if p.grad is not None:
+                    p.grad = p.grad.clone()
+        self._bucketer = self._make_bucketer(buckets)
+        self._has_rebuilt_buckets = True
+        self._ready_order = []
+
+    def _sync_bucket_indices(self, buckets):
+        """Broadcast rank 0's rebuilt layout (Reducer::sync_bucket_indices)."""
+        if self.world_size == 1:
+            return buckets
+        dev = self.device if self._backend == "nccl" else torch.device("cpu")
+        n = len(self._params)
+        flat = [len(buckets)] + [len(b) for b in buckets] + [i for b in buckets for i in b]
+        flat += [0] * (2 * n + 1 - len(flat))
+        t = torch.tensor(flat, dtype=torch.int64, device=dev)
+        src = dist.get_global_rank(self.process_group, 0) if self.process_group is not dist.group.WORLD else 0
+        dist.broadcast(t, src=src, group=self.process_group)
+        v = t.tolist()
+        nb = v[0]
+        counts = v[1:1 + nb]
+        out, pos = [], 1 + nb
+        for c in counts:
+            out.append(v[pos:pos + c])
+            pos += c
+        return out
+
+    # ------------------------------------------------------------------ API
+    def register_comm_hook(self, state: object, hook: Callable):
+        """hook(state, GradBucket) -> torch.futures.Future[Tensor] (T:nn/parallel/distributed.py:1953)."""
+        if self._comm_hook is not None:
+            raise RuntimeError("register_comm_hook or register_builtin_comm_hook can only be called once.")
+        if not callable(hook):
+            raise TypeError("Communication hook must be callable.")
+        self._comm_hook = (state, hook)
+        self._bucketer = self._make_bucketer(self._bucketer.buckets)
+
+    def set_grad_sqnorm_target(self, t: torch.Tensor | None):
+        """Fuse Σg² of the averaged grads into the unpack (fp32 1-element tensor)."""
+        self._sqnorm_target = t
+
+    def bucket_comm_ms(self):
+        """Per-bucket collective time of the last iteration (HIP events on the comm stream)."""
+        out = []
+        for bi in range(len(self._bucketer.buckets)):
+            ms = ctypes.c_float()
+            L.check(L.lib().gs_bucketer_last_comm_ms(self._bucketer.handle, bi, ctypes.byref(ms)),
+                    "gs_bucketer_last_comm_ms")
+            out.append(ms.value)
+        return out
+
+    def _get_ddp_logging_data(self):
+        b = self._bucketer
+        return {
+            "world_size": self.world_size,
+            "rank": self.rank,
+            "backend_name": "rccl(libgsync)" if self._comm is not None else self._backend,
+            "bucket_cap_bytes": self.bucket_bytes_cap,
+            "find_unused_parameters": int(self.find_unused_parameters),
+            "gradient_as_bucket_view": int(self.gradient_as_bucket_view),
+            "static_graph": int(self.static_graph),
+            "comm_hook": "" if self._comm_hook is None else getattr(self._comm_hook[1], "__qualname__", "hook"),
+            "has_rebuilt_buckets": int(self._has_rebuilt_buckets),
+            "bucket_sizes": b.logical_bytes(),
+            "rebuilt_bucket_sizes": b.logical_bytes() if self._has_rebuilt_buckets else [],
+            "padded_bucket_numels": [buf.numel() for buf in b.buffers],
+            "bucket_dtype": str(self._bucket_dtype),
+            "num_parameter_tensors": len(self._params),
+            "total_parameter_size_bytes": sum(p.numel() * p.element_size() for p in self._params),
+        }
+
+    def bucket_indices(self):
+        return [list(b) for b in self._bucketer.buckets]
+
+    def __del__(self):
+        for h in getattr(self, "_hook_handles", []):
+            try:
+                h.remove()
+            except Exception:  # pragma: no cover
+                pass
+
+
+DDP = DistributedDataParallel

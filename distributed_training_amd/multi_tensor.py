@@ -1,0 +1,161 @@
+"""Python handle on a libgsync multi-tensor plan (``gs_plan``).
+
+A plan is a static list of tensor sizes laid out in one flat buffer, with the
+work decomposition (segments / tasks) built once; only the per-tensor pointer
+tables change from call to call, and they are re-uploaded only when they do.
+It plays the role of ATen's ``multi_tensor_apply`` launch machinery
+(T:include/ATen/native/cuda/MultiTensorApply.cuh:14-21) for every op on the
+gradient-sync path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import _lib as L
+
+
+class TensorListPlan:
+    def __init__(self, numels: Sequence[int], device: torch.device, align: int = 0):
+        self.device = torch.device(device)
+        self.kind = L.GS_DEV_HIP if self.device.type == "cuda" else L.GS_DEV_HOST
+        self.numels = [int(n) for n in numels]
+        self.n = len(self.numels)
+        dev_index = self.device.index if self.device.index is not None else (
+            torch.cuda.current_device() if self.kind == L.GS_DEV_HIP else 0
+        )
+        self.dev_index = dev_index
+        h = ctypes.c_void_p()
+        lib = L.lib()
+        L.check(
+            lib.gs_plan_create(self.kind, dev_index, self.n, L.i64_array(self.numels), int(align), ctypes.byref(h)),
+            "gs_plan_create",
+        )
+        self.handle = h
+        self.flat_numel = int(lib.gs_plan_flat_numel(h))
+        offs = (ctypes.c_int64 * max(1, self.n))()
+        L.check(lib.gs_plan_offsets(h, offs), "gs_plan_offsets")
+        self.offsets = [int(offs[i]) for i in range(self.n)]
+        self._slot_cache: dict[int, tuple] = {}
+
+    # ------------------------------------------------------------------
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                L.lib().gs_plan_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+    def _stream(self, stream):
+        if stream is not None:
+            return stream
+        return L.stream_ptr(self.device)
+
+    def set_ptrs(self, slot: int, tensors_or_ptrs):
+        ptrs = tuple(
+            (t if isinstance(t, int) or t is None else t.data_ptr()) for t in tensors_or_ptrs
+        )
+        if len(ptrs) != self.n:
+            raise ValueError(f"plan has {self.n} tensors, got {len(ptrs)} pointers")
+        if self._slot_cache.get(slot) == ptrs:
+            return
+        L.check(L.lib().gs_plan_set_ptrs(self.handle, slot, L.ptr_array(ptrs), None), "gs_plan_set_ptrs")
+        self._slot_cache[slot] = ptrs
+
+    # ------------------------------------------------------------------ ops
+    def pack(self, src_slot, src_dtype, flat: torch.Tensor, scale=1.0, mode=L.GS_SCALE_NONE, stream=None):
+        L.check(
+            L.lib().gs_pack(self.handle, src_slot, L.gs_dtype(src_dtype), flat.data_ptr(),
+                            L.gs_dtype(flat.dtype), float(scale), mode, self._stream(stream)),
+            "gs_pack",
+        )
+
+    def unpack(self, flat: torch.Tensor, dst_slot, dst_dtype, sqnorm: torch.Tensor | None = None,
+               accumulate=False, stream=None):
+        L.check(
+            L.lib().gs_unpack(self.handle, flat.data_ptr(), L.gs_dtype(flat.dtype), dst_slot,
+                              L.gs_dtype(dst_dtype), None if sqnorm is None else sqnorm.data_ptr(),
+                              int(bool(accumulate)), self._stream(stream)),
+            "gs_unpack",
+        )
+
+    def scale(self, slot, dtype, s, mode=L.GS_SCALE_MUL, stream=None):
+        L.check(L.lib().gs_scale(self.handle, slot, L.gs_dtype(dtype), float(s), mode, self._stream(stream)),
+                "gs_scale")
+
+    def sqnorm(self, slot, dtype, out: torch.Tensor, accumulate=False, stream=None):
+        L.check(
+            L.lib().gs_sqnorm(self.handle, slot, L.gs_dtype(dtype), out.data_ptr(), int(bool(accumulate)),
+                              self._stream(stream)),
+            "gs_sqnorm",
+        )
+
+    def unscale_check(self, slot, dtype, inv_scale: torch.Tensor | None, found_inf: torch.Tensor, stream=None):
+        L.check(
+            L.lib().gs_unscale_check(self.handle, slot, L.gs_dtype(dtype),
+                                     None if inv_scale is None else inv_scale.data_ptr(),
+                                     found_inf.data_ptr(), self._stream(stream)),
+            "gs_unscale_check",
+        )
+
+    def sgd(self, grad_dtype, lr, momentum, dampening, weight_decay, nesterov, maximize, first_step,
+            lowp_dtype=None, grad_scale=None, found_inf=None, stream=None):
+        L.check(
+            L.lib().gs_sgd_step(
+                self.handle, L.gs_dtype(grad_dtype), -1 if lowp_dtype is None else L.gs_dtype(lowp_dtype),
+                float(lr), float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)),
+                int(bool(maximize)), int(bool(first_step)),
+                None if grad_scale is None else grad_scale.data_ptr(),
+                None if found_inf is None else found_inf.data_ptr(), self._stream(stream)),
+            "gs_sgd_step",
+        )
+
+    def adam(self, grad_dtype, lr, beta1, beta2, eps, weight_decay, adamw, maximize, step_size,
+             bias_correction2_sqrt, lowp_dtype=None, grad_scale=None, found_inf=None, stream=None):
+        L.check(
+            L.lib().gs_adam_step(
+                self.handle, L.gs_dtype(grad_dtype), -1 if lowp_dtype is None else L.gs_dtype(lowp_dtype),
+                float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(bool(adamw)),
+                int(bool(maximize)), float(step_size), float(bias_correction2_sqrt),
+                None if grad_scale is None else grad_scale.data_ptr(),
+                None if found_inf is None else found_inf.data_ptr(), self._stream(stream)),
+            "gs_adam_step",
+        )
+
+
+def clip_coef(sqnorm: torch.Tensor, max_norm: float, eps: float, coef: torch.Tensor,
+              norm: torch.Tensor | None = None, stream=None):
+    kind = L.GS_DEV_HIP if sqnorm.device.type == "cuda" else L.GS_DEV_HOST
+    if stream is None:
+        stream = L.stream_ptr(sqnorm.device)
+    L.check(
+        L.lib().gs_clip_coef(kind, sqnorm.data_ptr(), float(max_norm), float(eps), coef.data_ptr(),
+                             None if norm is None else norm.data_ptr(), stream),
+        "gs_clip_coef",
+    )
+
+
+def is_dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: the elements fill exactly numel() consecutive
+    slots starting at data_ptr() (any dim order, e.g. channels_last)."""
+    if t.is_contiguous():
+        return True
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.size()) if sz != 1)
+    expected = 1
+    for st, sz in dims:
+        if st != expected:
+            return False
+        expected *= sz
+    return True
+
+
+def dense_like_param(grad: torch.Tensor, param: torch.Tensor) -> bool:
+    """grad's memory is one dense block in the same element order as param's."""
+    return grad.shape == param.shape and grad.stride() == param.stride() and is_dense(grad)

@@ -1,0 +1,287 @@
+"""Fused multi-tensor optimizers on libgsync kernels (drop-ins for torch.optim).
+
+* :class:`FusedSGD`  — ``torch.optim.SGD`` semantics (T:optim/sgd.py:322-381
+  ``_single_tensor_sgd``; :383-470 ``_multi_tensor_sgd``): one HIP pass over
+  (param, grad, momentum_buffer) = 20 B/param fp32 instead of >=3 foreach passes.
+* :class:`FusedAdam` — ``torch.optim.Adam`` / ``AdamW`` semantics
+  (T:optim/adam.py:554-800 ``_multi_tensor_adam``, the reference's default on
+  GPU, ``R:resnet/pytorch_ddp/ddp_train.py:97``): one pass over
+  (p, g, m, v) = 28 B/param instead of the ~72 B/param of 7 foreach passes.
+* :func:`clip_grad_norm_` — ``torch.nn.utils.clip_grad_norm_``
+  (T:nn/utils/clip_grad.py:50-186) with a wave-level Σg² reduction and the
+  clip coefficient kept on the device (no host sync).
+
+``state_dict`` layouts are torch's (``momentum_buffer``; ``step`` /
+``exp_avg`` / ``exp_avg_sq``), so checkpoints move between the two.
+
+Extras used by the engine: ``grad_scale`` (a 1-element device tensor the
+update multiplies grads by — clip coefficient or AMP 1/scale), ``found_inf``
+(skip the step when non-zero) and ``max_grad_norm`` (DeepSpeed-style
+``gradient_clipping``: Σg² + coefficient computed on device, folded into the
+update kernel).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable
+
+import torch
+
+from . import _lib as L
+from .multi_tensor import TensorListPlan, clip_coef, is_dense
+
+
+def _group_key(tensors):
+    return tuple((t.data_ptr(), t.numel()) for t in tensors)
+
+
+class _PlanCache:
+    """One TensorListPlan per (param list, grad dtype) signature."""
+
+    def __init__(self):
+        self._plans: dict = {}
+
+    def get(self, params):
+        key = tuple(id(p) for p in params) + (params[0].device,)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = TensorListPlan([p.numel() for p in params], params[0].device)
+            self._plans[key] = plan
+        return plan
+
+
+def _check_dense(p: torch.Tensor, g: torch.Tensor, what: str):
+    if not is_dense(p):
+        raise RuntimeError(f"{what}: parameters must be dense (got strides {p.stride()})")
+    if g.stride() != p.stride() or not is_dense(g):
+        raise RuntimeError(f"{what}: grad layout must match its parameter's (param {p.stride()}, grad {g.stride()})")
+
+
+class _FusedBase(torch.optim.Optimizer):
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self._plans = _PlanCache()
+        self.grad_scale: torch.Tensor | None = None
+        self.found_inf: torch.Tensor | None = None
+        self._clip_buf: dict = {}
+
+    def _clip_scale(self, device, all_plans):
+        """DeepSpeed-style gradient_clipping folded into the update: returns the
+        device coefficient min(1, max_norm/(‖g‖+1e-6)) (times grad_scale)."""
+        max_norm = self.defaults.get("max_grad_norm")
+        if not max_norm:
+            return self.grad_scale
+        buf = self._clip_buf.get(device)
+        if buf is None:
+            buf = torch.zeros(3, dtype=torch.float32, device=device)
+            self._clip_buf[device] = buf
+        sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
+        for i, (plan, gdt) in enumerate(all_plans):
+            plan.sqnorm(1, gdt, sq, accumulate=i > 0)
+        if self.grad_scale is not None:
+            # norm of the unscaled grads: ‖g·s‖² = s²‖g‖²
+            sq.mul_(self.grad_scale * self.grad_scale)
+        clip_coef(sq, float(max_norm), 1e-6, coef, norm)
+        self.last_grad_norm = norm
+        if self.grad_scale is not None:
+            coef.mul_(self.grad_scale)
+        return coef
+
+
+class FusedSGD(_FusedBase):
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+                 *, maximize=False, foreach=None, differentiable=False, fused=None, max_grad_norm=None):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if momentum < 0.0:
+            raise ValueError(f"Invalid momentum value: {momentum}")
+        if weight_decay < 0.0:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        if differentiable:
+            raise ValueError("FusedSGD does not support differentiable=True")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov, maximize=maximize, foreach=foreach, differentiable=False,
+                        fused=fused, max_grad_norm=max_grad_norm)
+        super().__init__(params, defaults)
+
+    def _collect(self, group):
+        out = {}  # (grad dtype, has_buf) -> lists
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse:
+                raise RuntimeError("FusedSGD does not support sparse gradients")
+            _check_dense(p, p.grad, "FusedSGD")
+            if p.dtype != torch.float32:
+                raise RuntimeError("FusedSGD expects fp32 parameters (keep a fp32 master copy)")
+            st = self.state[p]
+            buf = st.get("momentum_buffer")
+            first = group["momentum"] != 0 and buf is None
+            if group["momentum"] != 0 and buf is None:
+                buf = torch.empty_like(p, memory_format=torch.preserve_format)
+                st["momentum_buffer"] = buf
+            key = (p.grad.dtype, first)
+            out.setdefault(key, ([], [], []))
+            ps, gs, bs = out[key]
+            ps.append(p)
+            gs.append(p.grad)
+            bs.append(buf)
+        return out
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        work = []
+        for group in self.param_groups:
+            for (gdt, first), (ps, gs, bs) in self._collect(group).items():
+                plan = self._plans.get(ps)
+                plan.set_ptrs(0, ps)
+                plan.set_ptrs(1, gs)
+                plan.set_ptrs(2, [b.data_ptr() if b is not None else 0 for b in bs])
+                work.append((group, plan, gdt, first))
+        if not work:
+            return loss
+        scale = self._clip_scale(work[0][1].device, [(w[1], w[2]) for w in work])
+        for group, plan, gdt, first in work:
+            plan.sgd(gdt, group["lr"], group["momentum"], group["dampening"], group["weight_decay"],
+                     group["nesterov"], group["maximize"], first, grad_scale=scale, found_inf=self.found_inf)
+        return loss
+
+
+class FusedAdam(_FusedBase):
+    """Adam (``adamw=False``) or AdamW (``adamw=True`` / ``decoupled_weight_decay=True``)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
+                 *, foreach=None, maximize=False, capturable=False, differentiable=False, fused=None,
+                 decoupled_weight_decay=False, adamw=None, max_grad_norm=None):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        if amsgrad:
+            raise NotImplementedError("FusedAdam: amsgrad is not on the reference path")
+        if differentiable:
+            raise ValueError("FusedAdam does not support differentiable=True")
+        adamw = bool(decoupled_weight_decay if adamw is None else adamw)
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        foreach=foreach, maximize=maximize, capturable=False, differentiable=False,
+                        fused=fused, decoupled_weight_decay=adamw, max_grad_norm=max_grad_norm)
+        super().__init__(params, defaults)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        work = []
+        for group in self.param_groups:
+            buckets = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                _check_dense(p, p.grad, "FusedAdam")
+                if p.dtype != torch.float32:
+                    raise RuntimeError("FusedAdam expects fp32 parameters (keep a fp32 master copy)")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                key = (p.grad.dtype, float(st["step"].item()))
+                lists = buckets.setdefault(key, ([], [], [], []))
+                lists[0].append(p)
+                lists[1].append(p.grad)
+                lists[2].append(st["exp_avg"])
+                lists[3].append(st["exp_avg_sq"])
+            for (gdt, step), (ps, gs, ms, vs) in buckets.items():
+                plan = self._plans.get(ps)
+                plan.set_ptrs(0, ps)
+                plan.set_ptrs(1, gs)
+                plan.set_ptrs(2, ms)
+                plan.set_ptrs(3, vs)
+                work.append((group, plan, gdt, step))
+        if not work:
+            return loss
+        scale = self._clip_scale(work[0][1].device, [(w[1], w[2]) for w in work])
+        for group, plan, gdt, step in work:
+            beta1, beta2 = group["betas"]
+            lr = group["lr"]
+            # python-double bias corrections, as torch's foreach path computes them
+            bias_correction1 = 1 - beta1 ** step
+            bias_correction2 = 1 - beta2 ** step
+            step_size = (lr / bias_correction1) * -1
+            bias_correction2_sqrt = bias_correction2 ** 0.5
+            plan.adam(gdt, lr, beta1, beta2, group["eps"], group["weight_decay"],
+                      group["decoupled_weight_decay"], group["maximize"], step_size, bias_correction2_sqrt,
+                      grad_scale=scale, found_inf=self.found_inf)
+        return loss
+
+
+class FusedAdamW(FusedAdam):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, **kw):
+        kw.pop("decoupled_weight_decay", None)
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=True, **kw)
+
+
+_NORM_PLANS: dict = {}
+
+
+@torch.no_grad()
+def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm: float, norm_type: float = 2.0,
+                    error_if_nonfinite: bool = False, foreach=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ for the L2 norm on libgsync kernels.
+
+    total_norm = ‖concat(g)‖₂ ; coef = min(1, max_norm / (total_norm + 1e-6));
+    grads *= coef (T:nn/utils/clip_grad.py:165-174).  Everything stays on the
+    device; only error_if_nonfinite forces a host read, as in torch.
+    """
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if float(norm_type) != 2.0:
+        raise NotImplementedError("clip_grad_norm_: only norm_type=2 is on the gradient-sync path")
+    if len(grads) == 0:
+        return torch.tensor(0.0)
+    dev = grads[0].device
+    groups: dict = {}
+    for g in grads:
+        if not is_dense(g):
+            raise RuntimeError("clip_grad_norm_: grads must be dense")
+        groups.setdefault(g.dtype, []).append(g)
+    buf = torch.zeros(3, dtype=torch.float32, device=dev)
+    sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
+    plans = []
+    for i, (dt, gl) in enumerate(groups.items()):
+        key = tuple(id(g) for g in gl) + (dev,)
+        plan = _NORM_PLANS.get(key)
+        if plan is None:
+            plan = TensorListPlan([g.numel() for g in gl], dev)
+            if len(_NORM_PLANS) > 64:
+                _NORM_PLANS.clear()
+            _NORM_PLANS[key] = plan
+        plan.set_ptrs(0, gl)
+        plan.sqnorm(0, dt, sq, accumulate=i > 0)
+        plans.append((plan, dt))
+    clip_coef(sq, float(max_norm), 1e-6, coef, norm)
+    if error_if_nonfinite and not torch.isfinite(norm).item():
+        raise RuntimeError(
+            f"The total norm of order {float(norm_type)} for gradients from `parameters` is non-finite, "
+            "so it cannot be clipped. To disable this error and scale the gradients by the non-finite "
+            "norm anyway, set `error_if_nonfinite=False`")
+    for plan, dt in plans:
+        # grads *= coef: a unit-scale SGD step is not the right tool; use the
+        # unscale kernel with the coefficient as the (device) multiplier
+        found = torch.zeros(1, dtype=torch.float32, device=dev)
+        plan.unscale_check(0, dt, coef, found)
+    return norm.reshape(())

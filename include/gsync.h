@@ -1,0 +1,246 @@
+/*
+ * gsync.h — C-ABI of libgsync, the MI355X-native data-parallel
+ * gradient-synchronisation engine (bucketer + RCCL collectives + fused
+ * multi-tensor optimizer) behind the reference's DDP / ZeRO training wrappers.
+ *
+ * Every entry point replaces a native piece of the reference's path (the
+ * reference itself is Python; its hot path lives in torch's c10d Reducer,
+ * ProcessGroupNCCL and the ATen foreach/fused optimizer kernels — see
+ * SURVEY.md §2.4 / §8a).  The "replaces:" line on each declaration names the
+ * reference-side interface (file:line; R: = /root/reference,
+ * T: = torch 2.10 under dist-packages/torch).
+ *
+ * Conventions
+ *   - every function returns int: 0 = ok, <0 = error (GS_E*); the message is
+ *     in gs_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *   - device memory is owned by the caller (torch caching allocator); the
+ *     library only receives raw pointers.  The library owns communicators,
+ *     streams, events and its own small metadata tables.
+ *   - `stream` arguments are hipStream_t passed as void* (NULL = legacy
+ *     default stream).  No entry point synchronises the host with the device
+ *     except *_destroy and gs_comm_create.
+ *   - device_kind GS_DEV_HIP runs hand-written gfx950 kernels; GS_DEV_HOST
+ *     runs the host implementation used for CPU tensors (the gloo/CPU
+ *     config).  A HIP plan never falls back to the host implementation.
+ */
+#ifndef GSYNC_H
+#define GSYNC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSYNC_VERSION 1000 /* 0.1.0 */
+
+/* ---- error codes ---- */
+#define GS_OK 0
+#define GS_EINVAL (-1)   /* bad argument (TORCH_CHECK equivalent) */
+#define GS_EHIP (-2)     /* HIP runtime error */
+#define GS_ERCCL (-3)    /* RCCL error */
+#define GS_ESTATE (-4)   /* call out of protocol order (Reducer REDUCER_CHECK equivalent) */
+#define GS_ENOMEM (-5)
+#define GS_ENODEV (-6)   /* HIP requested but no device / library built without it */
+
+/* ---- dtypes ---- */
+#define GS_F32 0
+#define GS_BF16 1
+#define GS_F16 2
+#define GS_F64 3
+#define GS_I64 4
+#define GS_I32 5
+#define GS_U8 6
+
+/* ---- device kinds ---- */
+#define GS_DEV_HOST 0
+#define GS_DEV_HIP 1
+
+/* ---- reduce ops (ncclRedOp_t order) ---- */
+#define GS_SUM 0
+#define GS_PROD 1
+#define GS_MAX 2
+#define GS_MIN 3
+#define GS_AVG 4
+
+/* ---- scale modes for pack / scale ---- */
+#define GS_SCALE_NONE 0
+#define GS_SCALE_MUL 1 /* x * s  — Reducer pack: at::mul_out(bucket_view, grad, 1/div_factor) */
+#define GS_SCALE_DIV 2 /* x / s  — Reducer view mode: bucket_view.div_(div_factor) */
+
+typedef struct gs_comm gs_comm;
+typedef struct gs_plan gs_plan;
+typedef struct gs_bucketer gs_bucketer;
+
+/* ======================================================================
+ * library
+ * ==================================================================== */
+int gs_version(void);
+const char* gs_last_error(void);
+/* number of HIP devices visible (0 on a CPU-only host) */
+int gs_device_count(void);
+
+/* ======================================================================
+ * communicator: RCCL over xGMI with a library-owned stream
+ * replaces: T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp:849
+ *           (allreduce), :836 (broadcast), :872 (_allgather_base),
+ *           :887-892 (reduce_scatter / _reduce_scatter_base),
+ *           per-device NCCL streams ncclStreams_ :1398
+ * ==================================================================== */
+int gs_comm_unique_id_bytes(void); /* 128 */
+int gs_comm_get_unique_id(uint8_t* out /* [gs_comm_unique_id_bytes()] */);
+int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm** out);
+int gs_comm_destroy(gs_comm* c);
+/* ncclCommAbort: for the failure path (timeout / peer death) */
+int gs_comm_abort(gs_comm* c);
+int gs_comm_rank(gs_comm* c);
+int gs_comm_world(gs_comm* c);
+/* the dedicated collective stream (hipStream_t) */
+int gs_comm_stream(gs_comm* c, void** stream_out);
+/* make `waiter` wait for all work queued so far on `signaler` (event edge) */
+int gs_stream_wait(void* waiter, void* signaler);
+
+/* collectives; stream NULL = the comm's own stream.  count in elements. */
+int gs_allreduce(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
+                 void* stream);
+int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,
+                      int op, void* stream);
+int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
+                  void* stream);
+int gs_broadcast(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
+                 void* stream);
+
+/* ======================================================================
+ * multi-tensor plan: a static list of tensor shapes laid out in one flat
+ * buffer (per-tensor offsets aligned to `align_elems`, 0 = packed back to
+ * back like torch's _flatten_dense_tensors / Reducer bucket), plus up to
+ * GS_PLAN_SLOTS per-tensor pointer tables (param / grad / state...).
+ * The work decomposition (segments + tasks) is built once on the host and
+ * uploaded once; pointer tables are re-uploaded only when they change.
+ * replaces: T:include/ATen/native/cuda/MultiTensorApply.cuh:14-21 launch
+ *           geometry (kILP 4, 64Ki-element chunks, <=110 tensors/launch)
+ * ==================================================================== */
+#define GS_PLAN_SLOTS 5
+int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* numels,
+                   int64_t align_elems, gs_plan** out);
+int gs_plan_destroy(gs_plan* p);
+int64_t gs_plan_flat_numel(gs_plan* p);
+int gs_plan_offsets(gs_plan* p, int64_t* out /* [n_tensors] */);
+int gs_plan_n_tasks(gs_plan* p);
+/* register the per-tensor pointers of one slot (uploads on change, ordered on `stream`) */
+int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* stream);
+
+/* flatten + fused scale + dtype cast: flat[off_t + i] = cast(src_t[i] (*|/) scale)
+ * replaces: Reducer::mark_variable_ready_dense (T:.../c10d/reducer.hpp:275,
+ *           upstream at::mul_out(bucket_view, grad, 1/div_factor_));
+ *           T:_utils.py:558 _flatten_dense_tensors */
+int gs_pack(gs_plan* p, int src_slot, int src_dtype, void* flat, int flat_dtype, float scale,
+            int scale_mode, void* stream);
+/* unflatten + cast: dst_t[i] = cast(flat[off_t + i]); if sqnorm_dev != NULL,
+ * Σ dst² (fp32) is written (accumulate=0) or added (accumulate=1) to sqnorm_dev[0]
+ * replaces: Reducer::copy_bucket_to_grad / finalize_bucket_dense (T:reducer.hpp:283,329);
+ *           T:_utils.py:578 _unflatten_dense_tensors */
+int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
+              float* sqnorm_dev, int accumulate, void* stream);
+/* in-place x = x (*|/) s on one slot (view-mode bucket_view.div_(div_factor)) */
+int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* stream);
+/* Σ x² over all tensors of one slot into sqnorm_dev[0] (fp32, deterministic order)
+ * replaces: T:nn/utils/clip_grad.py:96 torch._foreach_norm (+ vector_norm of norms) */
+int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate, void* stream);
+/* coef_dev[0] = min(1, max_norm / (sqrt(sqnorm_dev[0]) + eps)); norm_dev (nullable) = sqrt
+ * replaces: T:nn/utils/clip_grad.py:165-174 clip_coef / clamp */
+int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,
+                 float* coef_dev, float* norm_dev, void* stream);
+/* found_inf_dev[0] = 1.0 if any non-finite in slot, and (if inv_scale_dev) x *= inv_scale
+ * replaces: T:amp/grad_scaler.py:280 _amp_foreach_non_finite_check_and_unscale_ */
+int gs_unscale_check(gs_plan* p, int slot, int dtype, const float* inv_scale_dev,
+                     float* found_inf_dev, void* stream);
+
+/* fused SGD momentum / weight decay, one pass over (p, g, buf[, p_lowp]):
+ *   g' = g*gscale (+ wd*p);  buf = first ? g' : mom*buf + (1-damp)*g';
+ *   d = nesterov ? g' + mom*buf : buf;  p -= lr*d;  p_lowp = cast(p)
+ * slots: 0 = param (f32), 1 = grad (grad_dtype), 2 = momentum buffer (f32, unused if mom==0),
+ *        3 = optional low-precision param copy (lowp_dtype, -1 = none)
+ * grad_scale_dev (nullable): multiplies g (clip coefficient / AMP unscale);
+ * found_inf_dev (nullable): skip the whole step when *found_inf != 0.
+ * replaces: T:optim/sgd.py:322-381 _single_tensor_sgd, :383-470 _multi_tensor_sgd */
+int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double momentum,
+                double dampening, double weight_decay, int nesterov, int maximize, int first_step,
+                const float* grad_scale_dev, const float* found_inf_dev, void* stream);
+/* fused Adam / AdamW, one pass over (p, g, m, v[, p_lowp]) with torch's foreach arithmetic:
+ *   (adamw) p *= 1 - lr*wd  |  (adam) g += wd*p
+ *   m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
+ *   p += step_size * m / (sqrt(v)/bc2_sqrt + eps)       (step_size = -lr/bc1)
+ * slots: 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = optional low-precision copy
+ * Hyper-parameters are Python floats (double) and are rounded to fp32 exactly
+ * where torch rounds them: 1-b1, 1-b2, 1-lr*wd are formed in double first.
+ * replaces: T:optim/adam.py:554-800 _multi_tensor_adam (reference GPU default);
+ *           T:include/ATen/native/cuda/fused_adam_utils.cuh:11-88 */
+int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double beta1,
+                 double beta2, double eps, double weight_decay, int adamw, int maximize,
+                 double step_size, double bias_correction2_sqrt, const float* grad_scale_dev,
+                 const float* found_inf_dev, void* stream);
+
+/* ======================================================================
+ * bucket assignment (greedy by size per dtype, first-bucket cap)
+ * replaces: T:.../c10d/reducer.hpp:590-595 compute_bucket_assignment_by_size
+ *           (dist._compute_bucket_assignment_by_size)
+ * order: NULL -> tensors in index order and buckets sorted by min index;
+ *        else the gradient-ready order (no sort), as Reducer::rebuild_buckets.
+ * Writes bucket_of[n] (bucket id per tensor position in `order`/index order) and
+ * returns the bucket count (>=0) or an error.
+ * ==================================================================== */
+int gs_compute_bucket_assignment(int n, const int64_t* nbytes, const int32_t* dtype_keys,
+                                 const int32_t* order, int n_limits, const int64_t* limits,
+                                 int32_t* bucket_of /* [n], indexed by tensor id */,
+                                 int32_t* bucket_members /* [n] concatenated, bucket order */,
+                                 int32_t* bucket_counts /* [n] */);
+
+/* ======================================================================
+ * bucketer: the Reducer state machine
+ * replaces: T:.../c10d/reducer.hpp:52-63 Reducer ctor, :73 autograd_hook,
+ *           :275 mark_variable_ready_dense, :111-116 run_comm_hook,
+ *           :283 finalize_bucket_dense, :346-402 Bucket
+ * ==================================================================== */
+#define GS_BKT_AUTO_COLLECTIVE 1 /* library launches the collective itself (needs comm) */
+#define GS_BKT_GRAD_VIEW 2       /* grads already alias the bucket: scale in place, no unpack */
+#define GS_BKT_NO_SCALE 4        /* a comm hook owns the averaging: copy without 1/ws */
+#define GS_BKT_REDUCE_SCATTER 8  /* ZeRO-2: reduce-scatter into shard buffers instead of allreduce */
+#define GS_BKT_NO_UNPACK 16      /* caller consumes the bucket directly (ZeRO / fused step) */
+
+int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
+                       const int64_t* numels, int grad_dtype, int n_buckets,
+                       const int32_t* bucket_counts, const int32_t* bucket_members,
+                       int bucket_dtype, int64_t align_elems, float div_factor, int flags,
+                       gs_bucketer** out);
+int gs_bucketer_destroy(gs_bucketer* b);
+int gs_bucketer_bucket_numel(gs_bucketer* b, int bucket, int64_t* out);
+/* padded numel of the reduce-scatter output shard for a bucket (ZeRO-2) */
+int gs_bucketer_shard_numel(gs_bucketer* b, int bucket, int64_t* out);
+int gs_bucketer_param_location(gs_bucketer* b, int param, int32_t* bucket, int64_t* offset);
+/* storage for bucket `bucket` (torch-owned, bucket_numel elements of bucket_dtype) */
+int gs_bucketer_set_bucket_buffer(gs_bucketer* b, int bucket, void* ptr);
+/* ZeRO-2 output shard storage for bucket */
+int gs_bucketer_set_shard_buffer(gs_bucketer* b, int bucket, void* ptr);
+/* start of a backward pass that will synchronise (Reducer::prepare_for_backward).
+ * sqnorm_dev (nullable): receives Σ g² of the averaged grads, fused into unpack. */
+int gs_bucketer_prepare(gs_bucketer* b, float* sqnorm_dev);
+/* autograd hook: param's grad (grad_ptr) is final for this backward.
+ * ready_out[*n_ready] receives the buckets that became launchable, in launch
+ * order; with GS_BKT_AUTO_COLLECTIVE their collectives are already enqueued. */
+int gs_bucketer_mark_ready(gs_bucketer* b, int param, const void* grad, void* stream,
+                           int32_t* ready_out, int32_t* n_ready);
+/* mark every not-yet-ready param as unused (zero its slot) — find_unused_parameters */
+int gs_bucketer_mark_unused(gs_bucketer* b, void* stream, int32_t* ready_out, int32_t* n_ready);
+/* end of backward: unpack (unless view / no-unpack) and order `stream` after
+ * the collectives (Reducer::finalize_backward). */
+int gs_bucketer_finalize(gs_bucketer* b, void* stream);
+/* unpack one bucket (external-collective mode: after the caller's collective) */
+int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
+/* timing of the library's own collective launches (ms of the last iteration, via events) */
+int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSYNC_H */
