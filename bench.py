@@ -1,0 +1,227 @@
+"""Headline benchmark: ResNet-50 synthetic DDP training on MI355X with the
+libgsync gradient-sync engine (BASELINE.json metric "images/sec (node)
+ResNet-50 at 1/2/4/8 MI355X; grad-sync bus GB/s").
+
+One step = forward (bf16 autocast, channels_last) + backward with the
+libgsync bucketer packing/all-reducing/unpacking buckets on its own RCCL
+stream under backward + fused SGD-momentum/WD update, on 256 synthetic
+224x224 images per GPU generated on the device once (inputs resident in HBM).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+`roofline` for the dominant grad-sync kernel (the fused SGD update:
+20 B/param algorithmic, timed with HIP events on the stream it runs on),
+`grad_sync` (RCCL bus bandwidth of the bucket all-reduces, events on the
+libgsync comm stream, against (n-1) x 153 GB/s xGMI) and `cpu_baseline`
+(the reference's torch-DDP/gloo path on the host cores, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+XGMI_LINK_GBPS = 153.0  # per point-to-point link; bus roofline (n-1) x 153
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50", choices=["resnet18", "resnet50", "resnet152"])
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--bucket-cap-mb", type=float, default=None)
+    ap.add_argument("--bucket-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam"])
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--cudnn-benchmark", type=int, default=1)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU/gloo reference path (rank 0, N=1)")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+
+    import distributed_training_amd as D
+    from distributed_training_amd.resnet import MODELS
+
+    classes = 1000
+    torch.manual_seed(0)
+    model = MODELS[args.model](num_classes=classes).to(dev)
+    mf = torch.contiguous_format if args.no_channels_last else torch.channels_last
+    model = model.to(memory_format=mf)
+    bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
+    ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype)
+    if args.optimizer == "sgd":
+        opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
+    else:
+        opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world)
+        bytes_per_param = 28
+    n_params = sum(p.numel() for p in model.parameters())
+    grad_bytes = n_params * (2 if bucket_dtype is not None else 4)
+
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=mf)
+    y = torch.randint(0, classes, (args.batch,), device=dev, generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+
+    ev_opt = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = ddp(x)
+            loss = crit(out, y)
+        loss.backward()
+        if i is not None:
+            ev_opt[i][0].record()
+        opt.step()
+        if i is not None:
+            ev_opt[i][1].record()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    t_w0 = time.time()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    warm_s = time.time() - t_w0
+
+    comm_ms = []
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+        if world > 1 and i == args.steps - 1:
+            pass
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    if world > 1:
+        comm_ms = ddp.bucket_comm_ms()  # last iteration, per bucket (HIP events on the comm stream)
+
+    opt_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
+    opt_ms_avg = sum(opt_ms) / len(opt_ms)
+    img_s = world * args.batch * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    achieved = bytes_per_param * n_params / (opt_ms_avg * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            key = f"{args.model}/{args.optimizer}"
+            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    log = ddp._get_ddp_logging_data()
+    bucket_bytes = [b.numel() * b.element_size() for b in ddp._bucketer.buffers]
+    grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
+    if world > 1 and comm_ms and min(comm_ms) > 0:
+        tot_ms = sum(comm_ms)
+        bus = sum(bucket_bytes) / (tot_ms * 1e-3) * 2 * (world - 1) / world / 1e9
+        peak = (world - 1) * XGMI_LINK_GBPS
+        grad_sync.update({"allreduce_ms_per_step": tot_ms, "allreduce_bus_GBps": bus, "xgmi_peak_GBps": peak,
+                          "frac": bus / peak, "per_bucket_ms": comm_ms})
+    line = {
+        "metric": "images/sec (node) ResNet-50 at 1/2/4/8 MI355X; grad-sync bus GB/s",
+        "value": img_s,
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
+        "config": {
+            "workload": f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+                        f"libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
+                        f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}",
+            "global_batch": args.batch * world,
+            "per_gpu_batch": args.batch,
+            "parallelism": f"dp{world}",
+            "bucket_cap_mb": 25 if args.bucket_cap_mb is None else args.bucket_cap_mb,
+            "bucket_dtype": args.bucket_dtype,
+            "channels_last": not args.no_channels_last,
+            "params": n_params,
+        },
+        "roofline": {
+            "kernel": f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_per_param * n_params,
+            "avg_launch_ms": opt_ms_avg,
+            "median_launch_ms": opt_ms[len(opt_ms) // 2],
+        },
+        "grad_sync": grad_sync,
+        "warmup_s": warm_s,
+        "has_rebuilt_buckets": log["has_rebuilt_buckets"],
+    }
+    if args.cpu_baseline and world == 1:
+        from oracle.cpu_ddp_baseline import run as cpu_run
+
+        cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        cb = cpu_run(model=args.model, batch=16, ws=2, cores=cores, steps=3, warmup=1, port=_free_port())
+        line["cpu_baseline"] = {
+            "value": cb["images_per_sec"],
+            "unit": "images/sec",
+            "cores": cb["cores"],
+            "kind": "port",
+            "sample": f"torch DDP+gloo {args.model} 224x224, Adam(lr=1e-3*ws), ws=2 x 16 img/rank, "
+                      f"1 warmup + 3 timed steps (restates R:resnet/pytorch_ddp/ddp_train.py:79-114 on CPU)",
+        }
+    print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,100 @@
+"""CPU baseline: the reference's DDP training path on host cores.
+
+TEST / MEASUREMENT INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).  It
+restates R:resnet/pytorch_ddp/ddp_train.py:79-114 with the two changes
+BASELINE.md prescribes: backend "gloo" and no .cuda(); the model is wrapped
+in torch's own DistributedDataParallel and stepped with the reference's
+Adam(lr=1e-3*ws) through the reference's train-step body (:62-72), on
+synthetic data (seed 1234+rank).
+
+Prints one JSON line: {"images_per_sec": ..., "cores": ..., ...}
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def worker(rank, args, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(args.port)
+    dist.init_process_group("gloo", rank=rank, world_size=args.ws)  # :84 with gloo
+    torch.set_num_threads(max(1, args.cores // args.ws))
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from distributed_training_amd.resnet import MODELS
+
+    hw = 32 if args.model == "resnet18" else 224
+    classes = 10 if args.model == "resnet18" else 1000
+    torch.manual_seed(0)
+    model = DDP(MODELS[args.model](num_classes=classes))  # :95 without .cuda()
+    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3 * args.ws)  # :97, :110
+    criterion = nn.CrossEntropyLoss()
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.rand(args.batch, 3, hw, hw, generator=g)
+    y = torch.randint(0, classes, (args.batch,), generator=g)
+    model.train()
+    times = []
+    for it in range(args.warmup + args.steps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        outputs = model(x)                       # :66
+        loss = criterion(outputs, y)             # :67
+        loss.backward()                          # :70
+        optimizer.step()                         # :71
+        optimizer.zero_grad()                    # :72
+        loss.item()                              # :75
+        dist.barrier()
+        if it >= args.warmup:
+            times.append(time.perf_counter() - t0)
+    if rank == 0:
+        q.put(times)
+    dist.destroy_process_group()
+
+
+def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29777):
+    if cores is None:
+        cores = min(16, os.cpu_count() or 1)
+    args = argparse.Namespace(model=model, batch=batch, ws=ws, cores=cores, steps=steps, warmup=warmup, port=port)
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=worker, args=(r, args, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    times = q.get()
+    mean = sum(times) / len(times)
+    return {
+        "images_per_sec": ws * batch / mean,
+        "step_s": mean,
+        "cores": cores,
+        "ws": ws,
+        "batch_per_rank": batch,
+        "steps": steps,
+        "model": model,
+    }
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--ws", type=int, default=2)
+    ap.add_argument("--cores", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--port", type=int, default=29777)
+    a = ap.parse_args()
+    print(json.dumps(run(a.model, a.batch, a.ws, a.cores, a.steps, a.warmup, a.port)))
