@@ -115,9 +115,12 @@ def main():
         return loss
 
     t_w0 = time.time()
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        t_i = time.time()
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i}: {time.time() - t_i:.2f}s", file=sys.stderr, flush=True)
     warm_s = time.time() - t_w0
 
     comm_ms = []

@@ -58,6 +58,8 @@ def worker(rank, args, q):
         dist.barrier()
         if it >= args.warmup:
             times.append(time.perf_counter() - t0)
+        if rank == 0:
+            print(f"[cpu_baseline] step {it}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
     if rank == 0:
         q.put(times)
     dist.destroy_process_group()

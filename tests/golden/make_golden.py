@@ -202,7 +202,10 @@ def bucket_worker(rank, ws, port, out_path):
             log = ddp._get_ddp_logging_data()
             init_assign, init_limits = dist._compute_bucket_assignment_by_size(params, [2**62], [False] * len(params))
             rebuilt, _ = dist._compute_bucket_assignment_by_size(
-                params, [dist._DEFAULT_FIRST_BUCKET_BYTES, 25 * 1024 * 1024], [False] * len(params), first_order)
+                # Reducer::rebuild_buckets passes rebuilt_params_ (tensors in ready order)
+                # together with rebuilt_param_indices_
+                [params[i] for i in first_order], [dist._DEFAULT_FIRST_BUCKET_BYTES, 25 * 1024 * 1024],
+                [False] * len(params), first_order)
             out[f"{name}/{str(dtype).split('.')[-1]}"] = {
                 "numels": [p.numel() for p in params],
                 "element_size": params[0].element_size(),
