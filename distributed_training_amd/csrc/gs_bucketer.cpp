@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "gs_common.h"
@@ -216,7 +217,9 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     gs_bucketer_destroy(b);
     return rc;
   };
-  const int world = comm ? gs_comm_world(comm) : 1;
+  // div_factor is the world size (DDP / ZeRO divide by it); without a
+  // communicator (host / external collectives) it is the only source of it
+  const int world = comm ? gs_comm_world(comm) : std::max(1, static_cast<int>(div_factor + 0.5f));
   for (int bi = 0; bi < n_buckets; ++bi) {
     Bucket& bk = b->buckets[bi];
     std::vector<int64_t> nm;
@@ -232,8 +235,8 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     int rc = gs_plan_create(device_kind, device, static_cast<int>(nm.size()), nm.data(), align_elems, &bk.plan);
     if (rc != GS_OK) return bail(rc);
     bk.numel = bk.plan->flat_numel;
-    if (flags & GS_BKT_REDUCE_SCATTER) {
-      // pad so the bucket splits into `world` equal, aligned shards
+    if (flags & (GS_BKT_REDUCE_SCATTER | GS_BKT_NO_UNPACK)) {
+      // sharded consumers (ZeRO): pad so the bucket splits into `world` equal, aligned shards
       const int64_t q = static_cast<int64_t>(world) * (align_elems > 0 ? align_elems : 1);
       bk.numel = (bk.numel + q - 1) / q * q;
     }

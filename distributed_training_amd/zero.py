@@ -1,0 +1,362 @@
+"""ZeRO-1/2 data parallelism on libgsync (the DeepSpeed / ColossalAI
+LowLevelZero path; configured at
+R:resnet/deepspeed/deepspeed_train.py:210-219 and R:resnet/colossal/colossal_train.py:135-136).
+
+Layout (per bucket of <= reduce_bucket_size elements, DeepSpeed default 5e7 —
+one bucket for ResNet-18/50):
+
+  param flat (model dtype)  [ rank0 shard | rank1 shard | ... ]   params are views of it
+  grad bucket (model dtype) same layout; packed with the fused 1/ws scale
+  master (fp32)             this rank's shard only, plus exp_avg / exp_avg_sq
+
+backward: hooks pack each bucket and RCCL reduce-scatters it (stage 2) or
+          all-reduces it (stage 1) on libgsync's stream, under backward;
+step:     (fp16) non-finite check of the shard + MAX all-reduce of the flag,
+          (clip) Σg² of the shard + SUM all-reduce of one fp32 scalar,
+          coefficient on device; ONE fused Adam/SGD launch over all shards
+          that also writes the low-precision params into this rank's slice
+          of the param flat buffer; in-place all-gather of each bucket.
+No host synchronisation except the fp16 loss-scale bookkeeping (DeepSpeed
+reads its overflow flag on the host too).
+
+Parity: ZeRO-1/2 == DDP + the same optimizer (reduction order aside); the
+DeepSpeed/Colossal-specific numerics (AdamW mode, clip epsilon, loss scaling
+schedule) are restated from their published algorithms — DeepSpeed and
+ColossalAI are not installed here, so that part is "parity unpinned"
+(SURVEY.md §8c).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .comm import get_communicator
+from .ddp import BUCKET_ALIGN_ELEMS, compute_bucket_assignment_by_size
+from .multi_tensor import TensorListPlan, clip_coef, dense_like_param
+
+
+class DynamicLossScaler:
+    """DeepSpeed DynamicLossScaler semantics (loss_scale 0 = dynamic):
+    overflow -> (hysteresis) halve, floor at min_scale, skip the step;
+    `scale_window` clean steps -> double."""
+
+    def __init__(self, init_scale=2.0 ** 15, scale_window=500, hysteresis=2, min_scale=1.0, scale_factor=2.0,
+                 dynamic=True):
+        self.scale = float(init_scale)
+        self.scale_window = scale_window
+        self.hysteresis = hysteresis
+        self.cur_hysteresis = hysteresis
+        self.min_scale = min_scale
+        self.scale_factor = scale_factor
+        self.dynamic = dynamic
+        self.last_overflow_iter = -1
+        self.iter = 0
+
+    def update(self, overflow: bool):
+        if not self.dynamic:
+            self.iter += 1
+            return
+        if overflow:
+            if self.cur_hysteresis > 1:
+                self.cur_hysteresis -= 1
+            else:
+                self.scale = max(self.scale / self.scale_factor, self.min_scale)
+            self.last_overflow_iter = self.iter
+        elif (self.iter - self.last_overflow_iter) % self.scale_window == 0:
+            self.scale *= self.scale_factor
+            self.cur_hysteresis = self.hysteresis
+        self.iter += 1
+
+    def state_dict(self):
+        return dict(self.__dict__)
+
+    def load_state_dict(self, sd):
+        self.__dict__.update(sd)
+
+
+class ZeroDataParallel:
+    def __init__(self, module: torch.nn.Module, *, stage: int = 2, optimizer: str = "adamw", lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.0,
+                 process_group=None, reduce_bucket_size: int = int(5e7), gradient_clipping: float = 0.0,
+                 loss_scaler: DynamicLossScaler | None = None, broadcast_params: bool = True):
+        if stage not in (1, 2):
+            raise NotImplementedError(f"ZeRO stage {stage}: only 1 and 2 are on the gradient-sync path")
+        if not dist.is_initialized():
+            raise RuntimeError("ZeroDataParallel needs an initialised process group")
+        self.module = module
+        self.stage = stage
+        self.pg = process_group if process_group is not None else dist.group.WORLD
+        self.world = dist.get_world_size(self.pg)
+        self.rank = dist.get_rank(self.pg)
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        dts = {p.dtype for p in self.params}
+        if len(dts) != 1:
+            raise NotImplementedError(f"ZeRO: one parameter dtype expected, got {dts}")
+        self.dtype = next(iter(dts))
+        self.device = self.params[0].device
+        self.is_cuda = self.device.type == "cuda"
+        self.kind = optimizer
+        self.hp = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, momentum=momentum)
+        self.param_groups = [dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, momentum=momentum,
+                                  params=self.params)]
+        self.clip = float(gradient_clipping or 0.0)
+        self.scaler = loss_scaler
+        self.step_count = 0
+        self.require_backward_grad_sync = True
+        backend = dist.get_backend(self.pg)
+        self._comm = None
+        if self.is_cuda and backend == "nccl":
+            self._comm = get_communicator(None if self.pg is dist.group.WORLD else self.pg, self.device)
+        self._dev_index = self.device.index if self.device.index is not None else (
+            torch.cuda.current_device() if self.is_cuda else 0)
+
+        if broadcast_params and self.world > 1:
+            with torch.no_grad():
+                for t in list(self.params) + list(module.buffers()):
+                    self._bcast(t.data if t.is_floating_point() else t)
+
+        # buckets in gradient-ready (reverse module) order, <= reduce_bucket_size elements
+        n = len(self.params)
+        order = list(reversed(range(n)))
+        esz = self.params[0].element_size()
+        self.buckets = compute_bucket_assignment_by_size(self.params, [int(reduce_bucket_size) * esz], order=order)
+        self._make_bucketer()
+        self._build_flat_state()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.params)]
+        self._in_backward = False
+        self._queued = False
+        self._pending = {}
+        self._scratch = torch.zeros(4, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ setup
+    def _bcast(self, t):
+        if self._comm is not None:
+            self._comm.broadcast(t, 0, stream=L.stream_ptr(self.device))
+        else:
+            dist.broadcast(t, src=0, group=self.pg)
+
+    def _make_bucketer(self):
+        flags = L.GS_BKT_NO_UNPACK
+        if self._comm is not None:
+            flags |= L.GS_BKT_AUTO_COLLECTIVE
+            if self.stage == 2:
+                flags |= L.GS_BKT_REDUCE_SCATTER
+        kind = L.GS_DEV_HIP if self.is_cuda else L.GS_DEV_HOST
+        counts = [len(b) for b in self.buckets]
+        members = [i for b in self.buckets for i in b]
+        h = ctypes.c_void_p()
+        comm = self._comm.handle if self._comm is not None else None
+        # host / external-collective buckets are padded like reduce-scatter ones
+        L.check(L.lib().gs_bucketer_create(
+            comm, kind, self._dev_index, len(self.params), L.i64_array([p.numel() for p in self.params]),
+            L.gs_dtype(self.dtype), len(self.buckets), L.i32_array(counts), L.i32_array(members),
+            L.gs_dtype(self.dtype), BUCKET_ALIGN_ELEMS, float(self.world), flags, ctypes.byref(h)),
+            "gs_bucketer_create")
+        self.handle = h
+        self._ready = (ctypes.c_int32 * max(1, len(self.buckets)))()
+        self._n_ready = ctypes.c_int32()
+        q = self.world * BUCKET_ALIGN_ELEMS
+        self.bucket_numel, self.grad_bufs, self.grad_shards, self.loc = [], [], [], []
+        for b in range(len(self.buckets)):
+            nb = ctypes.c_int64()
+            L.check(L.lib().gs_bucketer_bucket_numel(h, b, ctypes.byref(nb)), "gs_bucketer_bucket_numel")
+            numel = nb.value
+            if numel % q:
+                raise RuntimeError("internal: bucket not padded to world*align")
+            buf = torch.zeros(numel, dtype=self.dtype, device=self.device)
+            L.check(L.lib().gs_bucketer_set_bucket_buffer(h, b, buf.data_ptr()), "set_bucket_buffer")
+            shard_n = numel // self.world
+            if flags & L.GS_BKT_REDUCE_SCATTER:
+                shard = torch.zeros(shard_n, dtype=self.dtype, device=self.device)
+                L.check(L.lib().gs_bucketer_set_shard_buffer(h, b, shard.data_ptr()), "set_shard_buffer")
+            else:
+                shard = buf[self.rank * shard_n:(self.rank + 1) * shard_n]
+            self.bucket_numel.append(numel)
+            self.grad_bufs.append(buf)
+            self.grad_shards.append(shard)
+        for i in range(len(self.params)):
+            bi, off = ctypes.c_int32(), ctypes.c_int64()
+            L.check(L.lib().gs_bucketer_param_location(h, i, ctypes.byref(bi), ctypes.byref(off)), "param_location")
+            self.loc.append((bi.value, off.value))
+
+    @torch.no_grad()
+    def _build_flat_state(self):
+        """params become views of per-bucket flat buffers; fp32 master shard + states."""
+        self.param_flats = []
+        for b, members in enumerate(self.buckets):
+            flat = torch.zeros(self.bucket_numel[b], dtype=self.dtype, device=self.device)
+            for i in members:
+                p = self.params[i]
+                _, off = self.loc[i]
+                view = flat.as_strided(p.size(), p.stride(), off)
+                view.copy_(p.data)
+                p.data = view
+            self.param_flats.append(flat)
+        shard_sizes = [n // self.world for n in self.bucket_numel]
+        self.shard_sizes = shard_sizes
+        self.param_shards = [f[self.rank * s:(self.rank + 1) * s] for f, s in zip(self.param_flats, shard_sizes)]
+        self.lowp = self.dtype != torch.float32
+        if self.lowp:
+            self.master = [ps.float().clone() for ps in self.param_shards]
+        else:
+            self.master = self.param_shards  # fp32 model: the shard IS the master copy
+        self.state1 = [torch.zeros(s, dtype=torch.float32, device=self.device) for s in shard_sizes]
+        self.state2 = [torch.zeros(s, dtype=torch.float32, device=self.device) for s in shard_sizes]
+        self.plan = TensorListPlan(shard_sizes, self.device)
+        self.plan.set_ptrs(0, self.master)
+        self.plan.set_ptrs(1, self.grad_shards)
+        self.plan.set_ptrs(2, self.state1)
+        if self.kind == "sgd":
+            self.plan.set_ptrs(3, self.param_shards if self.lowp else [0] * len(shard_sizes))
+        else:
+            self.plan.set_ptrs(3, self.state2)
+            self.plan.set_ptrs(4, self.param_shards if self.lowp else [0] * len(shard_sizes))
+
+    # ------------------------------------------------------------------ backward
+    def prepare_backward(self):
+        """Start a synchronising backward (called by the engine's backward())."""
+        if not self.require_backward_grad_sync:
+            self._in_backward = False
+            return
+        L.check(L.lib().gs_bucketer_prepare(self.handle, None), "gs_bucketer_prepare")
+        self._in_backward = True
+        self._queued = False
+        self._pending = {}
+        self._held = {}
+
+    def _make_hook(self, idx):
+        def hook(param):
+            if not self._in_backward:
+                return
+            if not self._queued:
+                self._queued = True
+                self._stream = L.stream_ptr(self.device)
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            g = param.grad
+            if not dense_like_param(g, param):
+                dense = torch.empty_like(param)
+                dense.copy_(g)
+                g = dense
+            # hold the grad until its bucket's pack is enqueued; param.grad is
+            # released now (DeepSpeed frees it too)
+            self._held.setdefault(self.loc[idx][0], []).append(g)
+            param.grad = None
+            L.check(L.lib().gs_bucketer_mark_ready(self.handle, idx, g.data_ptr(), self._stream, self._ready,
+                                                   ctypes.byref(self._n_ready)), "gs_bucketer_mark_ready")
+            for k in range(self._n_ready.value):
+                b = self._ready[k]
+                if self._comm is None:
+                    self._pending[b] = dist.all_reduce(self.grad_bufs[b], group=self.pg, async_op=True)
+                for held in self._held.pop(b, []):
+                    if self._comm is not None:
+                        # the pack on the comm stream is enqueued: the allocator may
+                        # reuse this memory only after it has run
+                        held.record_stream(self._comm.stream)
+
+        return hook
+
+    def _finalize(self):
+        for b in sorted(self._pending):
+            self._pending[b].wait()
+        self._pending = {}
+        L.check(L.lib().gs_bucketer_finalize(self.handle, self._stream), "gs_bucketer_finalize")
+        self._in_backward = False
+
+    # ------------------------------------------------------------------ step
+    def _allreduce_scalar(self, t, op):
+        if self._comm is not None:
+            self._comm.all_reduce(t, op=op, stream=L.stream_ptr(self.device))
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=self.pg)
+
+    @torch.no_grad()
+    def step(self):
+        s = self._scratch
+        found_inf = None
+        grad_scale = None
+        inv_scale = 1.0
+        if self.scaler is not None:
+            inv_scale = 1.0 / self.scaler.scale
+            found_inf = s[0:1]
+            found_inf.zero_()
+            self.plan.unscale_check(1, self.dtype, None, found_inf)
+            self._allreduce_scalar(found_inf, "max")
+        if self.clip > 0:
+            sq = s[1:2]
+            self.plan.sqnorm(1, self.dtype, sq)
+            self._allreduce_scalar(sq, "sum")
+            if inv_scale != 1.0:
+                sq.mul_(inv_scale * inv_scale)
+            clip_coef(sq, self.clip, 1e-6, s[2:3], s[3:4])
+            grad_scale = s[2:3]
+            if inv_scale != 1.0:
+                grad_scale.mul_(inv_scale)
+        elif inv_scale != 1.0:
+            grad_scale = s[2:3]
+            grad_scale.fill_(inv_scale)
+        g0 = self.param_groups[0]
+        lowp = self.dtype if self.lowp else None
+        self.step_count += 1
+        if self.kind == "sgd":
+            self.plan.sgd(self.dtype, g0["lr"], g0["momentum"], 0.0, g0["weight_decay"], False, False,
+                          self.step_count == 1, lowp_dtype=lowp, grad_scale=grad_scale, found_inf=found_inf)
+        else:
+            b1, b2 = g0["betas"]
+            bc1 = 1 - b1 ** self.step_count
+            bc2 = 1 - b2 ** self.step_count
+            self.plan.adam(self.dtype, g0["lr"], b1, b2, g0["eps"], g0["weight_decay"], self.kind == "adamw", False,
+                           (g0["lr"] / bc1) * -1, bc2 ** 0.5, lowp_dtype=lowp, grad_scale=grad_scale,
+                           found_inf=found_inf)
+        # re-replicate the updated parameters: in-place all-gather per bucket
+        for b, flat in enumerate(self.param_flats):
+            shard = self.param_shards[b]
+            if self._comm is not None:
+                self._comm.all_gather(shard, flat, stream=L.stream_ptr(self.device))
+            else:
+                chunks = list(flat.chunk(self.world))
+                dist.all_gather(chunks, shard.clone(), group=self.pg)
+        overflow = False
+        if self.scaler is not None:
+            overflow = bool(found_inf.item() != 0)  # DeepSpeed reads the overflow flag on the host
+            if overflow:
+                self.step_count -= 1
+            self.scaler.update(overflow)
+        return not overflow
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None
+
+    def grad_norm(self):
+        return self._scratch[3:4]
+
+    def state_dict(self):
+        return {"step": self.step_count, "rank": self.rank, "world": self.world,
+                "master": [m.detach().cpu() for m in self.master],
+                "exp_avg": [t.cpu() for t in self.state1], "exp_avg_sq": [t.cpu() for t in self.state2],
+                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
+                "loss_scaler": None if self.scaler is None else self.scaler.state_dict()}
+
+    def close(self):
+        for h in self._hooks:
+            h.remove()
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            L.lib().gs_bucketer_destroy(self.handle)
+            self.handle = None
+
+
+def warmup_lr(step: int, min_lr: float, max_lr: float, warmup_num_steps: int, warmup_type: str = "log") -> float:
+    """DeepSpeed WarmupLR (R:resnet/deepspeed/deepspeed_train.py:187-194): log (default) or linear
+    ramp from warmup_min_lr to warmup_max_lr over warmup_num_steps, then constant."""
+    if step < warmup_num_steps:
+        if warmup_type == "log":
+            gamma = math.log(step + 1) / math.log(warmup_num_steps) if warmup_num_steps > 1 else 1.0
+        else:
+            gamma = step / warmup_num_steps
+    else:
+        gamma = 1.0
+    return min_lr + (max_lr - min_lr) * gamma

@@ -1,0 +1,71 @@
+"""ZeRO-1/2 (libgsync ZeroDataParallel) on CPU/gloo, world_size 2 and 3:
+ZeRO == DDP + the same fused optimizer (SURVEY.md §8c pins the DeepSpeed /
+Colossal variants to this identity; reduction order is the same here, so it
+holds bit for bit), including gradient clipping and a bf16 model."""
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from tests.test_ddp_cpu import _micro, _run
+
+
+def _zero_vs_ddp(rank, ws, stage, kind, clip, dtype):
+    import distributed_training_amd as D
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    torch.manual_seed(0)
+    m1, m2 = _micro(), _micro()
+    m2.load_state_dict(m1.state_dict())
+    if dtype == "bf16":
+        m1 = m1.to(torch.bfloat16)
+    z = ZeroDataParallel(m1, stage=stage, optimizer=kind, lr=1e-2 if kind != "sgd" else 0.1, momentum=0.9,
+                         weight_decay=1e-4, gradient_clipping=clip, reduce_bucket_size=5000)
+    assert len(z.buckets) > 1  # several buckets at this cap
+    d = D.DistributedDataParallel(m2)
+    if kind == "sgd":
+        opt = D.FusedSGD(d.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, max_grad_norm=clip or None)
+    else:
+        opt = D.FusedAdam(d.parameters(), lr=1e-2, weight_decay=1e-4, adamw=kind == "adamw",
+                          max_grad_norm=clip or None)
+    g = torch.Generator().manual_seed(5 + rank)
+    for it in range(3):
+        x = torch.rand(4, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        z.prepare_backward()
+        nn.functional.cross_entropy(m1(x.to(m1.conv1.weight.dtype)).float(), y).backward()
+        z.step()
+        nn.functional.cross_entropy(d(x), y).backward()
+        opt.step()
+        opt.zero_grad()
+        for (n1, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+            if dtype == "bf16":
+                continue
+            if clip:
+                # Σg² is summed per shard then across ranks (vs whole-model in DDP):
+                # the clip coefficient may differ in the last bit
+                # (Adam tolerance of SURVEY §8c: atol = lr * 1e-3)
+                torch.testing.assert_close(p1.detach(), p2.detach(), rtol=0, atol=1e-2 * 1e-3)
+            else:
+                assert torch.equal(p1.detach(), p2.detach()), f"stage {stage} {kind} it {it} {n1}"
+    # every rank holds the full, identical parameters after the all-gather
+    w = torch.cat([p.detach().float().reshape(-1) for p in m1.parameters()])
+    allw = [torch.zeros_like(w) for _ in range(ws)]
+    dist.all_gather(allw, w)
+    for other in allw[1:]:
+        assert torch.equal(allw[0], other)
+    z.close()
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+@pytest.mark.parametrize("kind", ["adamw", "sgd"])
+def test_zero_equals_ddp_fp32(stage, kind):
+    _run(_zero_vs_ddp, 2, stage, kind, 0.0, "fp32")
+
+
+def test_zero_with_clipping_ws3():
+    _run(_zero_vs_ddp, 3, 2, "adamw", 0.5, "fp32")
+
+
+def test_zero_bf16_model_replicas_agree():
+    _run(_zero_vs_ddp, 2, 2, "adamw", 1.0, "bf16")
