@@ -1,12 +1,13 @@
 #!/bin/bash
-# One GPU session: tests, smoke, bench, rocprof stats.  Every GPU step has its
-# own time limit; a crash/abort/timeout (exit >= 2 for pytest, != 0 otherwise)
-# ends the session.
+# One GPU session: tests, smoke, bench, rocprof stats, PMC traffic.  Every GPU
+# step has its own time limit; a crash/abort/timeout ends the session.
+#   env: SKIP_TESTS=1 SKIP_BENCH=1 PROFILE=1 PMC=1 STEPS WARM BENCH_ARGS PYTEST_ARGS TAG
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
+TAG=${TAG:-r1}
 mkdir -p $OUT
-STEPS=${STEPS:-10}
+STEPS=${STEPS:-20}
 WARM=${WARM:-5}
 echo "== env"; python -c "import torch; print(torch.__version__, torch.cuda.get_device_name(0))" || exit 1
 echo "== lib identity"
@@ -29,13 +30,19 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 if [ "${SKIP_BENCH:-0}" != "1" ]; then
   echo "== bench"
-  timeout -k 10 600 python -u bench.py --gpus 1 --steps $STEPS --warmup $WARM ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
-  cat $OUT/bench.json
+  timeout -k 10 900 python -u bench.py --gpus 1 --steps $STEPS --warmup $WARM ${BENCH_ARGS:-} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
+  cat $OUT/bench_$TAG.json
 fi
+export TMPDIR=/tmp
 if [ "${PROFILE:-0}" == "1" ]; then
-  echo "== rocprofv3 kernel trace"
-  export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --gpus 1 --steps 5 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
-  find $OUT/prof -name "*stats*" | head
+  echo "== rocprofv3 kernel trace + stats (bench)"
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o bench -- python3 -u bench.py --gpus 1 --steps 5 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
+  find $OUT/prof_$TAG -name "*stats*"
+fi
+if [ "${PMC:-0}" == "1" ]; then
+  echo "== PMC traffic (separate passes)"
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 > $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+  python3 scripts/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG resnet50/sgd $OUT/pmc_traffic_$TAG.json
 fi
 echo "== done"

@@ -1,0 +1,26 @@
+"""Runs only the libgsync fused SGD kernel over the ResNet-50 parameter set
+(25.56M params in 161 tensors), N launches — the unit the PMC traffic pass
+measures (bench.py's roofline kernel)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_training_amd.multi_tensor import TensorListPlan  # noqa: E402
+from distributed_training_amd.resnet import MODELS  # noqa: E402
+
+model = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+dev = torch.device("cuda", 0)
+shapes = [p.shape for p in MODELS[model]().parameters()]
+ps = [torch.randn(s, device=dev) for s in shapes]
+gs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
+bs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
+plan = TensorListPlan([p.numel() for p in ps], dev)
+for k, ts in enumerate((ps, gs, bs)):
+    plan.set_ptrs(k, ts)
+for _ in range(iters):
+    plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)
+torch.cuda.synchronize()
+print("params", sum(p.numel() for p in ps), "launches", iters)
