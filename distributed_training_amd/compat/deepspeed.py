@@ -109,12 +109,13 @@ class WarmupLR:
         self.max_lr = warmup_max_lr
         self.warmup_num_steps = max(2, warmup_num_steps)
         self.warmup_type = warmup_type
+        # last_batch_iteration = index of the last completed optimizer step; the
+        # lr in the param groups is the one the NEXT step uses: warmup(last + 1)
         self.last_batch_iteration = last_batch_iteration
-        self._set(self.get_lr()[0] if last_batch_iteration >= 0 else warmup_lr(0, self.min_lr, self.max_lr,
-                                                                              self.warmup_num_steps, warmup_type))
+        self._set(self.get_lr()[0])
 
     def get_lr(self):
-        it = max(0, self.last_batch_iteration)
+        it = max(0, self.last_batch_iteration + 1)
         return [warmup_lr(it, self.min_lr, self.max_lr, self.warmup_num_steps, self.warmup_type)]
 
     def get_last_lr(self):

@@ -186,15 +186,75 @@ __device__ __forceinline__ float block_reduce(float v) {
 }
 
 // ------------------------------------------------------------- the engine
+// Everything a unit needs about its tensor, staged once per task in LDS
+// (one entry per segment of the task) instead of re-read from the global
+// tables for every unit.
+struct TV {
+  void* ptr[GS_PLAN_SLOTS];
+  int64_t numel;
+  int64_t off;
+  uint32_t align;
+  int32_t pad;
+  __device__ __forceinline__ bool vec(int slot) const { return (align >> slot) & 1u; }
+};
+
 // Op contract:
-//   struct Frag;                          registers for one unit
-//   bool active() const;                  uniform early-out (found_inf skip)
-//   void load(P, t, e, Frag&)             issue the unit's loads
-//   void apply(P, t, e, Frag&, float& acc) compute + store (+ reduction)
+//   struct Frag;                             registers for one unit (4 elements)
+//   bool active() const;                     uniform early-out (found_inf skip)
+//   void load(const TV&, e, Frag&)           issue the unit's loads
+//   void apply(const TV&, e, Frag&, acc)     compute + store (+ reduction)
 //   static constexpr int kRed = 0 (none) | 1 (sum) | 2 (max); float* partials
 template <int ILP, class Op>
+__device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
+                                          const int32_t* s_pref, int ns, int total, float& acc) {
+  if (ns == 1) {
+    // one (large) tensor segment: descriptor in registers, no per-unit search
+    const TV v = s_tv[0];
+    const int64_t ub = s_ubeg[0];
+    for (int base = 0; base < total; base += kBlock * ILP) {
+      typename Op::Frag f[ILP];
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+        if (u < total) op.load(v, (ub + u) * kUnit, f[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+        if (u < total) op.apply(v, (ub + u) * kUnit, f[j], acc);
+      }
+    }
+    return;
+  }
+  // many small tensors share the task: binary search in the LDS prefix
+  for (int base = 0; base < total; base += kBlock * ILP) {
+    typename Op::Frag f[ILP];
+    int kk[ILP];
+    int64_t ee[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+      kk[j] = -1;
+      if (u < total) {
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_pref[mid] <= u) lo = mid; else hi = mid - 1;
+        }
+        kk[j] = lo;
+        ee[j] = (s_ubeg[lo] + (u - s_pref[lo])) * kUnit;
+        op.load(s_tv[lo], ee[j], f[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j)
+      if (kk[j] >= 0) op.apply(s_tv[kk[j]], ee[j], f[j], acc);
+  }
+}
+
+template <int ILP, class Op>
 __global__ void __launch_bounds__(kBlock) mt_kernel(PlanArgs P, Op op) {
-  __shared__ int32_t s_tensor[kMaxSegPerTask];
+  __shared__ TV s_tv[kMaxSegPerTask];
   __shared__ int64_t s_ubeg[kMaxSegPerTask];
   __shared__ int32_t s_pref[kMaxSegPerTask + 1];
   float acc = 0.f;
@@ -204,40 +264,21 @@ __global__ void __launch_bounds__(kBlock) mt_kernel(PlanArgs P, Op op) {
     const int ns = P.task_begin[task + 1] - sb;
     if (threadIdx.x < ns) {
       const Seg sg = P.segs[sb + threadIdx.x];
-      s_tensor[threadIdx.x] = sg.tensor;
+      const int t = sg.tensor;
+      TV v;
+#pragma unroll
+      for (int s = 0; s < GS_PLAN_SLOTS; ++s) v.ptr[s] = P.ptrs[static_cast<int64_t>(s) * P.n + t];
+      v.numel = P.numel[t];
+      v.off = P.off[t];
+      v.align = P.align[t];
+      v.pad = 0;
+      s_tv[threadIdx.x] = v;
       s_ubeg[threadIdx.x] = sg.unit_begin;
       s_pref[threadIdx.x] = sg.task_off;
       if (threadIdx.x == ns - 1) s_pref[ns] = sg.task_off + sg.units;
     }
     __syncthreads();
-    const int total = s_pref[ns];
-    for (int base = 0; base < total; base += kBlock * ILP) {
-      typename Op::Frag f[ILP];
-      int tt[ILP];
-      int64_t ee[ILP];
-#pragma unroll
-      for (int j = 0; j < ILP; ++j) {
-        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
-        tt[j] = -1;
-        if (u < total) {
-          int k = 0;
-          if (ns > 1) {  // binary search in the LDS-staged prefix
-            int lo = 0, hi = ns - 1;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (s_pref[mid] <= u) lo = mid; else hi = mid - 1;
-            }
-            k = lo;
-          }
-          tt[j] = s_tensor[k];
-          ee[j] = (s_ubeg[k] + (u - s_pref[k])) * kUnit;
-          op.load(P, tt[j], ee[j], f[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < ILP; ++j)
-        if (tt[j] >= 0) op.apply(P, tt[j], ee[j], f[j], acc);
-    }
+    run_units<ILP>(op, s_tv, s_ubeg, s_pref, ns, s_pref[ns], acc);
     __syncthreads();
   }
   if constexpr (Op::kRed != 0) {
@@ -261,6 +302,11 @@ __global__ void __launch_bounds__(kBlock) combine_partials(const float* partials
 }
 
 // ---------------------------------------------------------------- ops
+template <int DT>
+__device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
+  return static_cast<char*>(flat) + off * (DT == GS_F32 ? 4 : 2);
+}
+
 template <int SD, int FD>
 struct PackOp {
   static constexpr int kRed = 0;
@@ -272,29 +318,27 @@ struct PackOp {
   int mode;
   struct Frag { float x[4]; };
   __device__ bool active() const { return true; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    const void* src = slot_ptr(P, slot, t);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    const void* src = v.ptr[slot];
     if (src == nullptr) {  // unused parameter (find_unused_parameters): pack zeros
       f.x[0] = f.x[1] = f.x[2] = f.x[3] = 0.f;
       return;
     }
-    load4<SD>(src, e, P.numel[t], slot_vec(P, slot, t), f.x);
+    load4<SD>(src, e, v.numel, v.vec(slot), f.x);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
-    const int64_t off = P.off[t];
+  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float v = f.x[i];
+      float x = f.x[i];
       if (mode == GS_SCALE_MUL) {
-        v = v * s;
+        x = x * s;
       } else if (mode == GS_SCALE_DIV) {
         // bf16_compress_hook order: round to the bucket dtype, then divide
-        v = round_to<FD>(v) / s;
+        x = round_to<FD>(x) / s;
       }
-      f.x[i] = v;
+      f.x[i] = x;
     }
-    char* fb = static_cast<char*>(flat) + off * (FD == GS_F32 ? 4 : 2);
-    store4<FD>(fb, e, P.numel[t], flat_vec && (off % kUnit) == 0, f.x);
+    store4<FD>(flat_at<FD>(flat, v.off), e, v.numel, flat_vec && (v.off % kUnit) == 0, f.x);
   }
 };
 
@@ -308,20 +352,19 @@ struct UnpackOp {
   int slot;
   struct Frag { float x[4]; };
   __device__ bool active() const { return true; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    const int64_t off = P.off[t];
-    const char* fb = static_cast<const char*>(flat) + off * (FD == GS_F32 ? 4 : 2);
-    load4<FD>(fb, e, P.numel[t], flat_vec && (off % kUnit) == 0, f.x);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    load4<FD>(flat_at<FD>(const_cast<void*>(flat), v.off), e, v.numel,
+              flat_vec && (v.off % kUnit) == 0, f.x);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float& acc) const {
-    void* dst = slot_ptr(P, slot, t);
+  __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
+    void* dst = v.ptr[slot];
     if (dst == nullptr) return;  // unused parameter: grad left untouched
-    store4<DD>(dst, e, P.numel[t], slot_vec(P, slot, t), f.x);
+    store4<DD>(dst, e, v.numel, v.vec(slot), f.x);
     if (want_sq) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float v = round_to<DD>(f.x[i]);
-        acc = fmaf(v, v, acc);
+        const float r = round_to<DD>(f.x[i]);
+        acc = fmaf(r, r, acc);
       }
     }
   }
@@ -336,13 +379,13 @@ struct ScaleOp {
   int mode;
   struct Frag { float x[4]; };
   __device__ bool active() const { return true; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
+  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
 #pragma unroll
     for (int i = 0; i < 4; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
-    store4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+    store4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
 };
 
@@ -353,10 +396,10 @@ struct SqnormOp {
   int slot;
   struct Frag { float x[4]; };
   __device__ bool active() const { return true; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
-  __device__ void apply(const PlanArgs&, int, int64_t, Frag& f, float& acc) const {
+  __device__ void apply(const TV&, int64_t, Frag& f, float& acc) const {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc = fmaf(f.x[i], f.x[i], acc);
   }
@@ -370,20 +413,19 @@ struct UnscaleOp {
   const float* inv;  // nullable
   struct Frag { float x[4]; };
   __device__ bool active() const { return true; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    load4<DT>(slot_ptr(P, slot, t), e, P.numel[t], slot_vec(P, slot, t), f.x);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float& acc) const {
-    const int64_t n = P.numel[t];
+  __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (e + i < n && !isfinite(f.x[i])) acc = 1.f;
+      if (e + i < v.numel && !isfinite(f.x[i])) acc = 1.f;
     if (inv) {
       const float s = *inv;
       if (s != 1.f) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) f.x[i] = f.x[i] * s;
-        store4<DT>(slot_ptr(P, slot, t), e, n, slot_vec(P, slot, t), f.x);
+        store4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
       }
     }
   }
@@ -399,14 +441,12 @@ struct SgdOp {
   const float* found_inf;
   struct Frag { float p[4], g[4], b[4]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    const int64_t n = P.numel[t];
-    load4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
-    load4<GD>(slot_ptr(P, 1, t), e, n, slot_vec(P, 1, t), f.g);
-    if (h.mom != 0.f && !h.first) load4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.b);
+  __device__ void load(const TV& v, int64_t e, Frag& f) const {
+    load4<GS_F32>(v.ptr[0], e, v.numel, v.vec(0), f.p);
+    load4<GD>(v.ptr[1], e, v.numel, v.vec(1), f.g);
+    if (h.mom != 0.f && !h.first) load4<GS_F32>(v.ptr[2], e, v.numel, v.vec(2), f.b);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
-    const int64_t n = P.numel[t];
+  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -423,9 +463,9 @@ struct SgdOp {
       }
       f.p[i] = fmaf(-h.lr, d, f.p[i]);              // param.add_(d, alpha=-lr)
     }
-    store4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
-    if (h.mom != 0.f) store4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.b);
-    if constexpr (LD >= 0) store4<LD>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.p);
+    store4<GS_F32>(v.ptr[0], e, v.numel, v.vec(0), f.p);
+    if (h.mom != 0.f) store4<GS_F32>(v.ptr[2], e, v.numel, v.vec(2), f.b);
+    if constexpr (LD >= 0) store4<LD>(v.ptr[3], e, v.numel, v.vec(3), f.p);
   }
 };
 
@@ -439,15 +479,13 @@ struct AdamOp {
   const float* found_inf;
   struct Frag { float p[4], g[4], m[4], v[4]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
-  __device__ void load(const PlanArgs& P, int t, int64_t e, Frag& f) const {
-    const int64_t n = P.numel[t];
-    load4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
-    load4<GD>(slot_ptr(P, 1, t), e, n, slot_vec(P, 1, t), f.g);
-    load4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.m);
-    load4<GS_F32>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.v);
+  __device__ void load(const TV& tv, int64_t e, Frag& f) const {
+    load4<GS_F32>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
+    load4<GD>(tv.ptr[1], e, tv.numel, tv.vec(1), f.g);
+    load4<GS_F32>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
+    load4<GS_F32>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
   }
-  __device__ void apply(const PlanArgs& P, int t, int64_t e, Frag& f, float&) const {
-    const int64_t n = P.numel[t];
+  __device__ void apply(const TV& tv, int64_t e, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -465,10 +503,10 @@ struct AdamOp {
       p = fmaf(h.step_size, m / denom, p);                  // addcdiv_(m, denom, -lr/bc1)
       f.p[i] = p; f.m[i] = m; f.v[i] = v;
     }
-    store4<GS_F32>(slot_ptr(P, 0, t), e, n, slot_vec(P, 0, t), f.p);
-    store4<GS_F32>(slot_ptr(P, 2, t), e, n, slot_vec(P, 2, t), f.m);
-    store4<GS_F32>(slot_ptr(P, 3, t), e, n, slot_vec(P, 3, t), f.v);
-    if constexpr (LD >= 0) store4<LD>(slot_ptr(P, 4, t), e, n, slot_vec(P, 4, t), f.p);
+    store4<GS_F32>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
+    store4<GS_F32>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
+    store4<GS_F32>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
+    if constexpr (LD >= 0) store4<LD>(tv.ptr[4], e, tv.numel, tv.vec(4), f.p);
   }
 };
 

@@ -39,10 +39,14 @@ def _run(fn, ws, *args):
 
 
 def _wrap(fn, rank, ws, port, errq, *args):
+    import faulthandler
+
+    faulthandler.enable(all_threads=True)
     try:
         init_pg("gloo", rank, ws, port)
         torch.set_num_threads(max(1, 8 // ws))  # as make_golden.py: CPU conv sums depend on it
         fn(rank, ws, *args)
+        dist.barrier()  # no rank tears gloo down while a peer is still talking
         dist.destroy_process_group()
     except BaseException as e:
         import traceback
