@@ -1,0 +1,184 @@
+"""ZeRO-1/2, AMP loss scaling and the DeepSpeed / Colossal shims on the GPU.
+
+* ws=1 over RCCL (AUTO reduce-scatter / all-reduce on libgsync's stream):
+  ZeRO == DDP + the same fused optimizer, bit for bit (fp32 model).
+* ws=2 sharing the box's one GPU (gloo carries the collectives, every
+  pack / update / cast is a HIP kernel): same identity, bit for bit.
+* GradScaler: libgsync's device-side unscale/skip vs torch.amp.GradScaler.
+"""
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+from tests._dist_util import free_port, init_pg
+from tests.test_compat_cpu import DS_CONFIG, SHIMS
+
+pytestmark = pytest.mark.gpu
+
+
+def _micro():
+    from distributed_training_amd.resnet import ResNet, BasicBlock
+
+    return ResNet(BasicBlock, [1, 1, 1, 1], num_classes=10, width=8)
+
+
+def _zero_vs_ddp(dev, rank, stage, kind, steps=3, collective="auto"):
+    import distributed_training_amd as D
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    torch.manual_seed(0)
+    m1, m2 = _micro().to(dev), _micro().to(dev)
+    m2.load_state_dict(m1.state_dict())
+    z = ZeroDataParallel(m1, stage=stage, optimizer=kind, lr=1e-2 if kind != "sgd" else 0.1, momentum=0.9,
+                         weight_decay=1e-4, reduce_bucket_size=30000)
+    d = D.DistributedDataParallel(m2, collective=collective)
+    if kind == "sgd":
+        opt = D.FusedSGD(d.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        opt = D.FusedAdam(d.parameters(), lr=1e-2, weight_decay=1e-4, adamw=kind == "adamw")
+    g = torch.Generator(device=dev).manual_seed(5 + rank)
+    for it in range(steps):
+        x = torch.rand(4, 3, 32, 32, device=dev, generator=g)
+        y = torch.randint(0, 10, (4,), device=dev, generator=g)
+        z.prepare_backward()
+        nn.functional.cross_entropy(m1(x), y).backward()
+        z.step()
+        nn.functional.cross_entropy(d(x), y).backward()
+        opt.step()
+        opt.zero_grad()
+        torch.cuda.synchronize()
+        for (n1, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+            assert torch.equal(p1.detach(), p2.detach()), f"stage {stage} {kind} it {it} {n1}"
+    z.close()
+
+
+@pytest.fixture(scope="module")
+def rccl_pg(cuda_device):
+    if dist.is_initialized():
+        yield
+        return
+    init_pg("nccl", 0, 1, free_port())
+    yield
+    from distributed_training_amd.comm import destroy_communicators
+
+    destroy_communicators()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+@pytest.mark.parametrize("kind", ["adamw", "sgd"])
+def test_zero_equals_ddp_ws1_rccl(cuda_device, rccl_pg, stage, kind):
+    _zero_vs_ddp(cuda_device, 0, stage, kind)
+
+
+def test_zero_bf16_model_ws1(cuda_device, rccl_pg):
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    torch.manual_seed(0)
+    m = _micro().to(cuda_device).to(torch.bfloat16)
+    z = ZeroDataParallel(m, stage=2, optimizer="adamw", lr=1e-3, gradient_clipping=1.0)
+    x = torch.rand(4, 3, 32, 32, device=cuda_device, dtype=torch.bfloat16)
+    y = torch.randint(0, 10, (4,), device=cuda_device)
+    before = [p.detach().clone() for p in m.parameters()]
+    for _ in range(2):
+        z.prepare_backward()
+        nn.functional.cross_entropy(m(x).float(), y).backward()
+        assert z.step()
+    torch.cuda.synchronize()
+    # bf16 params are the rounded fp32 master shard
+    for b, p, in zip(before, m.parameters()):
+        assert torch.isfinite(p.float()).all()
+    master = torch.cat(z.master)
+    flat = torch.cat([f[:n] for f, n in zip(z.param_flats, z.shard_sizes)])
+    assert torch.equal(master.to(torch.bfloat16), flat)
+    assert 0 < z.grad_norm().item() < 1e6
+    z.close()
+
+
+def _ws2_worker(rank, ws, port, errq):
+    try:
+        init_pg("gloo", rank, ws, port)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        for stage in (1, 2):
+            _zero_vs_ddp(dev, rank, stage, "adamw", steps=2, collective="process_group")
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        import traceback
+
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
+def test_zero_equals_ddp_ws2_one_gpu(cuda_device):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = free_port()
+    procs = [ctx.Process(target=_ws2_worker, args=(r, 2, port, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_grad_scaler_matches_torch(cuda_device):
+    from distributed_training_amd.amp import GradScaler
+    from distributed_training_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    m1, m2 = _micro().to(cuda_device), _micro().to(cuda_device)
+    m2.load_state_dict(m1.state_dict())
+    o1 = FusedAdam(m1.parameters(), lr=1e-3)
+    o2 = torch.optim.Adam(m2.parameters(), lr=1e-3)
+    s1 = GradScaler(init_scale=2.0 ** 10, growth_interval=2)
+    s2 = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, growth_interval=2)
+    x = torch.rand(4, 3, 32, 32, device=cuda_device)
+    y = torch.randint(0, 10, (4,), device=cuda_device)
+    for it in range(4):
+        for m, o, s in ((m1, o1, s1), (m2, o2, s2)):
+            with torch.autocast("cuda", dtype=torch.float16):
+                loss = nn.functional.cross_entropy(m(x), y)
+            s.scale(loss).backward()
+            if it == 2:  # poison one grad: the step must be skipped and the scale backed off
+                next(m.parameters()).grad[0].view(-1)[0] = float("inf")
+            s.step(o)
+            s.update()
+            o.zero_grad()
+        assert s1.get_scale() == s2.get_scale(), (it, s1.get_scale(), s2.get_scale())
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            torch.testing.assert_close(p1, p2, rtol=0, atol=1e-3 * 1e-3 * 4)
+
+
+def test_deepspeed_shim_gpu_bf16_stage2(cuda_device, rccl_pg):
+    sys.path.insert(0, SHIMS)
+    import copy
+
+    import deepspeed
+
+    cfg = copy.deepcopy(DS_CONFIG)
+    cfg["zero_optimization"]["stage"] = 2
+    cfg["bf16"]["enabled"] = True
+    cfg["train_batch_size"] = 8
+    torch.manual_seed(0)
+    model = _micro()
+    engine, _, _, _ = deepspeed.initialize(model=model, model_parameters=model.parameters(), config=cfg)
+    assert engine.bfloat16_enabled() and engine._zero is not None and engine._zero._comm is not None
+    x = torch.rand(8, 3, 32, 32, device=cuda_device).to(torch.bfloat16)
+    y = torch.randint(0, 10, (8,), device=cuda_device)
+    for _ in range(3):
+        loss = nn.CrossEntropyLoss()(model(x), y)
+        engine.backward(loss)
+        engine.step()
+    torch.cuda.synchronize()
+    assert engine.global_steps == 3
+    assert all(torch.isfinite(p.float()).all() for p in model.parameters())
