@@ -45,8 +45,11 @@ inline bool is_float_dtype(int dt) { return dt == GS_F32 || dt == GS_BF16 || dt 
 // <= kMaxSegPerTask segments; one workgroup processes one task at a time
 // (small tensors share a task; their descriptors are staged in LDS).
 constexpr int kUnit = 4;
-constexpr int kSegUnits = 4096;     // 16Ki elements = 64 KiB fp32 per stream
-constexpr int kTaskUnits = 4096;
+#ifndef GS_SEG_UNITS
+#define GS_SEG_UNITS 4096
+#endif
+constexpr int kSegUnits = GS_SEG_UNITS;   // 16Ki elements = 64 KiB fp32 per stream
+constexpr int kTaskUnits = GS_SEG_UNITS;
 constexpr int kMaxSegPerTask = 64;
 constexpr int kBlock = 256;         // 4 waves of 64
 constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups

@@ -90,6 +90,37 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
   return (GLOBAL_AS T*)(p);
 }
 
+// Build-time tuning knobs (defaults are the measured best)
+#ifndef GS_NT_LOAD
+#define GS_NT_LOAD 0
+#endif
+#ifndef GS_NT_STORE
+#define GS_NT_STORE 0
+#endif
+#ifndef GS_PACK_ILP
+#define GS_PACK_ILP 4
+#endif
+#ifndef GS_OPT_ILP
+#define GS_OPT_ILP 2
+#endif
+
+template <class V>
+__device__ __forceinline__ V vload(const GLOBAL_AS V* p) {
+#if GS_NT_LOAD
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class V>
+__device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
+#if GS_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // load 4 consecutive elements [e, e+4) of a tensor with n elements
 template <int DT>
 __device__ __forceinline__ void load4(const void* base, int64_t e, int64_t n, bool vec,
@@ -97,7 +128,7 @@ __device__ __forceinline__ void load4(const void* base, int64_t e, int64_t n, bo
   if constexpr (DT == GS_F32) {
     const GLOBAL_AS float* p = gptr<float>(base) + e;
     if (vec && e + 4 <= n) {
-      const gf4 v = *(const GLOBAL_AS gf4*)p;
+      const gf4 v = vload((const GLOBAL_AS gf4*)p);
       x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
     } else {
 #pragma unroll
@@ -106,7 +137,7 @@ __device__ __forceinline__ void load4(const void* base, int64_t e, int64_t n, bo
   } else {
     const GLOBAL_AS uint16_t* p = gptr<uint16_t>(base) + e;
     if (vec && e + 4 <= n) {
-      const gu2 v = *(const GLOBAL_AS gu2*)p;
+      const gu2 v = vload((const GLOBAL_AS gu2*)p);
       x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
       x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
       x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
@@ -126,7 +157,7 @@ __device__ __forceinline__ void store4(void* base, int64_t e, int64_t n, bool ve
     if (vec && e + 4 <= n) {
       gf4 v;
       v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
-      *(GLOBAL_AS gf4*)p = v;
+      vstore((GLOBAL_AS gf4*)p, v);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -140,7 +171,7 @@ __device__ __forceinline__ void store4(void* base, int64_t e, int64_t n, bool ve
             (static_cast<uint32_t>(from_f32<DT>(x[1])) << 16);
       v.y = static_cast<uint32_t>(from_f32<DT>(x[2])) |
             (static_cast<uint32_t>(from_f32<DT>(x[3])) << 16);
-      *(GLOBAL_AS gu2*)p = v;
+      vstore((GLOBAL_AS gu2*)p, v);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -686,7 +717,7 @@ int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, floa
   GS_DISPATCH_FLOAT(src_dt, SD, GS_DISPATCH_FLOAT(flat_dt, FD, {
     PackOp<SD, FD> op;
     op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s; op.mode = mode;
-    return launch<4>(p, op, stream);
+    return launch<GS_PACK_ILP>(p, op, stream);
   }));
   return GS_OK;
 }
@@ -697,7 +728,7 @@ int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_
   GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
     UnpackOp<FD, DD> op;
     op.want_sq = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
-    return launch<4>(p, op, stream, sq, acc);
+    return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
   }));
   return GS_OK;
 }
@@ -707,7 +738,7 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
     ScaleOp<DT> op;
     op.slot = slot; op.s = s; op.mode = mode;
-    return launch<4>(p, op, stream);
+    return launch<GS_PACK_ILP>(p, op, stream);
   });
   return GS_OK;
 }
@@ -717,7 +748,7 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
     SqnormOp<DT> op;
     op.slot = slot;
-    return launch<4>(p, op, stream, sq, acc);
+    return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
   });
   return GS_OK;
 }
@@ -737,7 +768,7 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
     UnscaleOp<DT> op;
     op.slot = slot; op.inv = inv;
     // found_inf accumulates (max) into the caller's flag, as torch's kernel does
-    return launch<4>(p, op, stream, found, 1);
+    return launch<GS_PACK_ILP>(p, op, stream, found, 1);
   });
   return GS_OK;
 }
@@ -748,7 +779,7 @@ int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, c
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     SgdOp<GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi;
-    return launch<2>(p, op, stream);
+    return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;
 }
@@ -759,7 +790,7 @@ int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc,
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     AdamOp<GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi;
-    return launch<2>(p, op, stream);
+    return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;
 }
