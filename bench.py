@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--bucket-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam"])
+    ap.add_argument("--engine", default="ddp", choices=["ddp", "zero1", "zero2"],
+                    help="ddp = headline (BASELINE configs[1-2]); zero1/zero2 = DeepSpeed-style (configs[3])")
     ap.add_argument("--no-channels-last", action="store_true")
     # MIOpen Find (benchmark=1) tunes every conv for minutes on a fresh box; the
     # immediate-mode solutions are what the 5.9k img/s number was measured with
@@ -86,15 +88,31 @@ def main():
     mf = torch.contiguous_format if args.no_channels_last else torch.channels_last
     model = model.to(memory_format=mf)
     bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
-    ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype)
-    if args.optimizer == "sgd":
-        opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
-    else:
-        opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world)
-        bytes_per_param = 28
     n_params = sum(p.numel() for p in model.parameters())
-    grad_bytes = n_params * (2 if bucket_dtype is not None else 4)
+    zero = None
+    if args.engine == "ddp":
+        ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype)
+        if args.optimizer == "sgd":
+            opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+            bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
+        else:
+            opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world)
+            bytes_per_param = 28
+        grad_bytes = n_params * (2 if bucket_dtype is not None else 4)
+    else:
+        # DeepSpeed-style ZeRO (BASELINE configs[3]): bf16 model, fp32 master shard,
+        # reduce-scatter (zero2) / all-reduce (zero1) of bf16 grads, AdamW, all-gather
+        from distributed_training_amd.zero import ZeroDataParallel
+
+        model = model.to(torch.bfloat16)
+        zero = ZeroDataParallel(model, stage=2 if args.engine == "zero2" else 1,
+                                optimizer="sgd" if args.optimizer == "sgd" else "adamw",
+                                lr=1e-3, momentum=0.9, weight_decay=3e-7, reduce_bucket_size=int(5e7),
+                                gradient_clipping=1.0)
+        ddp = model
+        # per shard param: p r/w fp32, g r bf16, states r/w fp32, bf16 param write
+        bytes_per_param = (4 + 4 + 2 + 8 + 2) if args.optimizer == "sgd" else (4 + 4 + 2 + 16 + 2)
+        grad_bytes = n_params * 2
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=mf)
@@ -103,7 +121,20 @@ def main():
 
     ev_opt = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
+    if zero is not None:
+        x = x.to(torch.bfloat16)
+
     def step(i=None):
+        if zero is not None:
+            zero.prepare_backward()
+            loss = crit(ddp(x).float(), y)
+            loss.backward()
+            if i is not None:
+                ev_opt[i][0].record()
+            zero.step()
+            if i is not None:
+                ev_opt[i][1].record()
+            return loss
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = ddp(x)
             loss = crit(out, y)
@@ -139,7 +170,7 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    if world > 1:
+    if world > 1 and zero is None:
         comm_ms = ddp.bucket_comm_ms()  # last iteration, per bucket (HIP events on the comm stream)
 
     opt_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
@@ -151,9 +182,10 @@ def main():
         dist.destroy_process_group()
         return
 
-    achieved = bytes_per_param * n_params / (opt_ms_avg * 1e-3) / 1e9
+    upd_params = n_params if zero is None else n_params // world  # ZeRO updates this rank's shard
+    achieved = bytes_per_param * upd_params / (opt_ms_avg * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(args.traffic_json) and zero is None:
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
@@ -161,8 +193,12 @@ def main():
             traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    log = ddp._get_ddp_logging_data()
-    bucket_bytes = [b.numel() * b.element_size() for b in ddp._bucketer.buffers]
+    if zero is None:
+        log = ddp._get_ddp_logging_data()
+        bucket_bytes = [b.numel() * b.element_size() for b in ddp._bucketer.buffers]
+    else:
+        log = {"has_rebuilt_buckets": 0}
+        bucket_bytes = [b.numel() * b.element_size() for b in zero.grad_bufs]
     grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
     if world > 1 and comm_ms and min(comm_ms) > 0:
         tot_ms = sum(comm_ms)
@@ -184,9 +220,14 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
         "config": {
-            "workload": f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
-                        f"libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
-                        f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}",
+            "workload": (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+                         f"libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
+                         f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}") if zero is None else
+                        (f"{args.model} synthetic 224x224 bf16 model training, {args.batch} img/GPU, libgsync "
+                         f"{args.engine.upper()} (bf16 {'reduce-scatter' if args.engine == 'zero2' else 'all-reduce'}"
+                         f" under backward, fp32 master shard, clip 1.0, fused "
+                         f"{'SGD' if args.optimizer == 'sgd' else 'AdamW'}, bf16 all-gather)"),
+            "engine": args.engine,
             "global_batch": args.batch * world,
             "per_gpu_batch": args.batch,
             "parallelism": f"dp{world}",
@@ -196,14 +237,15 @@ def main():
             "params": n_params,
         },
         "roofline": {
-            "kernel": f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)",
+            "kernel": (f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
+                       if zero is None else "ZeRO step window: shard Σg² + clip + fused update + all-gather"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_per_param * n_params,
+            "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
             "avg_launch_ms": opt_ms_avg,
             "median_launch_ms": opt_ms[len(opt_ms) // 2],
         },

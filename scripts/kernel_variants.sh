@@ -1,13 +1,19 @@
 #!/bin/bash
-# Time every libgsync build variant under distributed_training_amd/lib/variants
-set -u
+# Time libgsync build variants (interleaved, REPEAT rounds) with bench_kernels.py
+#   VARIANTS="libgsync variants/libgsync_v_old ..." (relative to distributed_training_amd/lib)
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-for lib in distributed_training_amd/lib/libgsync.so distributed_training_amd/lib/variants/*.so; do
-  name=$(basename $lib .so)
-  for m in "resnet50 1" "resnet152 2"; do
-    set -- $m
-    echo "== $name $1 x$2" | tee -a $OUT/kvariants.log
-    GSYNC_LIB=$lib timeout -k 10 200 python -u bench_kernels.py --model $1 --replicas $2 --skip-torch --iters 30 | sed "s/^/$name /" >> $OUT/kvariants.log 2>> $OUT/kvariants.err || exit 1
+VARIANTS=${VARIANTS:-"libgsync $(cd distributed_training_amd/lib && ls variants/*.so | sed 's/\.so$//' | tr '\n' ' ')"}
+for r in $(seq 1 ${REPEAT:-1}); do
+for v in $VARIANTS; do
+  lib=distributed_training_amd/lib/$v.so
+  name=$(basename $v)
+  MODELS=${MODELS:-resnet50:1 resnet152:2}
+  for m in $MODELS; do
+    mm=${m%%:*}; rep=${m#*:}
+    echo "== $name $mm x$rep round $r" | tee -a $OUT/kvariants.log
+    GSYNC_LIB=$lib timeout -k 10 200 python -u bench_kernels.py --model $mm --replicas $rep --skip-torch --iters 30 | sed "s/^/$name /" >> $OUT/kvariants.log 2>> $OUT/kvariants.err || exit 1
   done
+done
 done

@@ -27,32 +27,50 @@ def _micro():
 
 
 def _zero_vs_ddp(dev, rank, stage, kind, steps=3, collective="auto"):
-    import distributed_training_amd as D
-    from distributed_training_amd.zero import ZeroDataParallel
+    """ZeRO step == oracle(DDP average of the ranks' local grads, then the same
+    optimizer per element), bit for bit.  (MIOpen's backward is not
+    deterministic run to run, so the local grads are snapshotted by a hook
+    registered before ZeRO's and the expected weights come from the oracle.)"""
+    import numpy as np
 
+    from distributed_training_amd.zero import ZeroDataParallel
+    from oracle import oracle as O
+
+    ws = dist.get_world_size()
     torch.manual_seed(0)
-    m1, m2 = _micro().to(dev), _micro().to(dev)
-    m2.load_state_dict(m1.state_dict())
-    z = ZeroDataParallel(m1, stage=stage, optimizer=kind, lr=1e-2 if kind != "sgd" else 0.1, momentum=0.9,
-                         weight_decay=1e-4, reduce_bucket_size=30000)
-    d = D.DistributedDataParallel(m2, collective=collective)
-    if kind == "sgd":
-        opt = D.FusedSGD(d.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-    else:
-        opt = D.FusedAdam(d.parameters(), lr=1e-2, weight_decay=1e-4, adamw=kind == "adamw")
+    m1 = _micro().to(dev)
+    params = list(m1.parameters())
+    local = {}
+    for i, p in enumerate(params):
+        p.register_post_accumulate_grad_hook(lambda q, i=i: local.__setitem__(i, q.grad.detach().float().cpu().numpy()))
+    lr = 1e-2 if kind != "sgd" else 0.1
+    z = ZeroDataParallel(m1, stage=stage, optimizer=kind, lr=lr, momentum=0.9, weight_decay=1e-4,
+                         reduce_bucket_size=30000)
+    state = [None] * len(params)
     g = torch.Generator(device=dev).manual_seed(5 + rank)
     for it in range(steps):
         x = torch.rand(4, 3, 32, 32, device=dev, generator=g)
         y = torch.randint(0, 10, (4,), device=dev, generator=g)
+        before = [p.detach().float().cpu().numpy().reshape(-1) for p in params]
         z.prepare_backward()
         nn.functional.cross_entropy(m1(x), y).backward()
         z.step()
-        nn.functional.cross_entropy(d(x), y).backward()
-        opt.step()
-        opt.zero_grad()
         torch.cuda.synchronize()
-        for (n1, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
-            assert torch.equal(p1.detach(), p2.detach()), f"stage {stage} {kind} it {it} {n1}"
+        mine = [local[i] for i in range(len(params))]
+        allg = [None] * ws
+        dist.all_gather_object(allg, mine)
+        avg = O.ddp_average(allg)
+        for i, p in enumerate(params):
+            ga = avg[i].reshape(-1)
+            if kind == "sgd":
+                want, buf = O.sgd(before[i], ga, state[i], lr, 0.9, 0.0, 1e-4, False, False, state[i] is None)
+                state[i] = buf
+            else:
+                m, v = state[i] if state[i] is not None else (np.zeros_like(ga), np.zeros_like(ga))
+                want, m, v = O.adam(before[i], ga, m, v, it + 1, lr, 0.9, 0.999, 1e-8, 1e-4, kind == "adamw")
+                state[i] = (m, v)
+            got = p.detach().float().cpu().numpy().reshape(-1)
+            assert np.array_equal(got, want), f"stage {stage} {kind} it {it} param {i}"
     z.close()
 
 
@@ -133,13 +151,15 @@ def test_zero_equals_ddp_ws2_one_gpu(cuda_device):
 
 def test_grad_scaler_matches_torch(cuda_device):
     from distributed_training_amd.amp import GradScaler
-    from distributed_training_amd.optim import FusedAdam
+    from distributed_training_amd.optim import FusedSGD
 
     torch.manual_seed(0)
     m1, m2 = _micro().to(cuda_device), _micro().to(cuda_device)
     m2.load_state_dict(m1.state_dict())
-    o1 = FusedAdam(m1.parameters(), lr=1e-3)
-    o2 = torch.optim.Adam(m2.parameters(), lr=1e-3)
+    # SGD (linear in g): MIOpen's backward is not bit-reproducible between the two
+    # replicas, and Adam would amplify those last-bit differences into sign flips
+    o1 = FusedSGD(m1.parameters(), lr=1e-2, momentum=0.9)
+    o2 = torch.optim.SGD(m2.parameters(), lr=1e-2, momentum=0.9)
     s1 = GradScaler(init_scale=2.0 ** 10, growth_interval=2)
     s2 = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, growth_interval=2)
     x = torch.rand(4, 3, 32, 32, device=cuda_device)
@@ -156,7 +176,7 @@ def test_grad_scaler_matches_torch(cuda_device):
             o.zero_grad()
         assert s1.get_scale() == s2.get_scale(), (it, s1.get_scale(), s2.get_scale())
         for p1, p2 in zip(m1.parameters(), m2.parameters()):
-            torch.testing.assert_close(p1, p2, rtol=0, atol=1e-3 * 1e-3 * 4)
+            torch.testing.assert_close(p1, p2, rtol=1e-4, atol=1e-6)
 
 
 def test_deepspeed_shim_gpu_bf16_stage2(cuda_device, rccl_pg):
