@@ -65,6 +65,14 @@ class _FusedBase(torch.optim.Optimizer):
         self.found_inf: torch.Tensor | None = None
         self._clip_buf: dict = {}
 
+    def _skipped_on_host(self) -> bool:
+        """Host read of the AMP ``found_inf`` flag, for the cases a device-side
+        skip cannot express: torch skips ``optimizer.step()`` entirely on an
+        overflow (T:amp/grad_scaler.py ``_maybe_opt_step``), so a skipped step
+        must neither create momentum buffers (SGD's first step is buf = g) nor
+        advance Adam's step count (its bias corrections are host doubles)."""
+        return self.found_inf is not None and bool(self.found_inf.item() != 0)
+
     def _clip_scale(self, device, all_plans):
         """DeepSpeed-style gradient_clipping folded into the update: returns the
         device coefficient min(1, max_norm/(‖g‖+1e-6)) (times grad_scale)."""
@@ -136,6 +144,10 @@ class FusedSGD(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        new_bufs = any(group["momentum"] != 0 and p.grad is not None and "momentum_buffer" not in self.state[p]
+                       for group in self.param_groups for p in group["params"])
+        if new_bufs and self._skipped_on_host():
+            return loss
         work = []
         for group in self.param_groups:
             for (gdt, first), (ps, gs, bs) in self._collect(group).items():
@@ -181,6 +193,8 @@ class FusedAdam(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._skipped_on_host():
+            return loss
         work = []
         for group in self.param_groups:
             buckets = {}

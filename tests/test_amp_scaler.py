@@ -1,0 +1,82 @@
+"""libgsync GradScaler + fused optimizers vs torch.amp.GradScaler + torch.optim.
+
+Both sides step on the SAME gradients (model 1's backward, copied into model
+2's ``.grad``), so MIOpen's run-to-run backward differences never enter: what
+is compared is the scaler (unscale, overflow detection, skip, scale update)
+and the optimizer arithmetic only.  Overflows are injected on the first step
+(SGD momentum buffers must not be created by a skipped step; Adam's step count
+must not advance) and mid-run.
+
+Tolerances: SGD rtol 1e-6 / atol 1e-7 (fp32, fma placement may differ from
+ATen's in the last bit); Adam atol lr*1e-3 (its sign can flip
+where |g| ~ eps).
+"""
+import pytest
+import torch
+import torch.nn as nn
+
+from distributed_training_amd.amp import GradScaler
+from distributed_training_amd.optim import FusedAdam, FusedSGD
+
+
+def _micro():
+    from distributed_training_amd.resnet import ResNet, BasicBlock
+
+    return ResNet(BasicBlock, [1, 1, 1, 1], num_classes=10, width=8)
+
+
+def _run(dev, kind, poison_at, iters=5):
+    torch.manual_seed(0)
+    m1, m2 = _micro().to(dev), _micro().to(dev)
+    m2.load_state_dict(m1.state_dict())
+    if kind == "sgd":
+        o1 = FusedSGD(m1.parameters(), lr=1e-2, momentum=0.9, weight_decay=1e-4)
+        o2 = torch.optim.SGD(m2.parameters(), lr=1e-2, momentum=0.9, weight_decay=1e-4)
+        tol = dict(rtol=1e-6, atol=1e-7)
+    else:
+        o1 = FusedAdam(m1.parameters(), lr=1e-3)
+        o2 = torch.optim.Adam(m2.parameters(), lr=1e-3)
+        tol = dict(rtol=0, atol=1e-3 * 1e-3)
+    s1 = GradScaler(dev.type, init_scale=2.0 ** 10, growth_interval=2)
+    s2 = torch.amp.GradScaler(dev.type, init_scale=2.0 ** 10, growth_interval=2)
+    g = torch.Generator(device=dev).manual_seed(7)
+    for it in range(iters):
+        x = torch.rand(4, 3, 32, 32, device=dev, generator=g)
+        y = torch.randint(0, 10, (4,), device=dev, generator=g)
+        loss = nn.functional.cross_entropy(m1(x), y)
+        s1.scale(loss).backward()
+        s2.scale(loss.detach())  # lazy-inits torch's scale on the device
+        if it in poison_at:
+            next(m1.parameters()).grad.view(-1)[3] = float("inf")
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            p2.grad = p1.grad.detach().clone()
+        s1.step(o1)
+        s1.update()
+        s2.step(o2)
+        s2.update()
+        o1.zero_grad()
+        o2.zero_grad()
+        assert s1.get_scale() == s2.get_scale(), (it, s1.get_scale(), s2.get_scale())
+        for k, (p1, p2) in enumerate(zip(m1.parameters(), m2.parameters())):
+            torch.testing.assert_close(p1, p2, **tol, msg=lambda m: f"iter {it} param {k}: {m}")
+    # optimizer state layout and content follow torch's
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        st1, st2 = o1.state[p1], o2.state[p2]
+        assert set(st1) == set(st2)
+        if kind == "sgd":
+            torch.testing.assert_close(st1["momentum_buffer"], st2["momentum_buffer"], rtol=1e-6, atol=1e-7)
+        else:
+            assert float(st1["step"]) == float(st2["step"])
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("poison_at", [(0,), (2,), (0, 1, 3)])
+def test_scaler_cpu_host_backend(kind, poison_at):
+    _run(torch.device("cpu"), kind, poison_at)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("poison_at", [(0,), (2,), (0, 1, 3)])
+def test_scaler_gpu(cuda_device, kind, poison_at):
+    _run(cuda_device, kind, poison_at)
