@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--skip-torch", action="store_true")
+    ap.add_argument("--tag", default=os.environ.get("GSYNC_LIB", "libgsync").split("/")[-1])
     args = ap.parse_args()
     from distributed_training_amd.multi_tensor import TensorListPlan
     from distributed_training_amd.resnet import MODELS
@@ -71,6 +72,7 @@ def main():
     def rec(name, nbytes, ms_med, ms_avg, impl):
         gbs = nbytes / (ms_avg * 1e-3) / 1e9
         row = {"kernel": name, "impl": impl, "model": args.model, "replicas": args.replicas, "params": n,
+               "tag": args.tag, "task_units": plan.task_units, "n_tasks": plan.n_tasks,
                "alg_bytes": nbytes, "median_ms": ms_med, "avg_ms": ms_avg, "GBps": gbs, "frac_of_8TBps": gbs / HBM_PEAK}
         out.append(row)
         print(json.dumps(row), flush=True)

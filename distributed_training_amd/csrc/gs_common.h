@@ -40,16 +40,21 @@ inline int dtype_size(int dt) {
 inline bool is_float_dtype(int dt) { return dt == GS_F32 || dt == GS_BF16 || dt == GS_F16; }
 
 // ---- multi-tensor work decomposition ----
-// A tensor is cut into segments of <= kSegUnits units (1 unit = 4 elements).
-// Consecutive segments are grouped into tasks of <= kTaskUnits units and
+// A tensor is cut into segments of <= task_units units (1 unit = 4 elements;
+// plan_task_units() sizes them per plan, at most kSegUnits).
+// Consecutive segments are grouped into tasks of <= task_units units and
 // <= kMaxSegPerTask segments; one workgroup processes one task at a time
 // (small tensors share a task; their descriptors are staged in LDS).
 constexpr int kUnit = 4;
 #ifndef GS_SEG_UNITS
-#define GS_SEG_UNITS 4096
+#define GS_SEG_UNITS 16384
 #endif
-constexpr int kSegUnits = GS_SEG_UNITS;   // 16Ki elements = 64 KiB fp32 per stream
-constexpr int kTaskUnits = GS_SEG_UNITS;
+constexpr int kSegUnits = GS_SEG_UNITS;   // max task: 64Ki elements = 256 KiB fp32 per stream
+constexpr int kMinTaskUnits = 256;        // one unit per lane of a 256-thread workgroup
+#ifndef GS_TARGET_TASKS
+#define GS_TARGET_TASKS 1920
+#endif
+constexpr int kTargetTasks = GS_TARGET_TASKS;  // < kMaxGrid: ragged tensor ends add tasks
 constexpr int kMaxSegPerTask = 64;
 constexpr int kBlock = 256;         // 4 waves of 64
 constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups
@@ -110,6 +115,7 @@ struct gs_plan {
   std::vector<gs::Seg> segs;
   std::vector<int32_t> task_begin;
   int grid = 0;
+  int64_t task_units = 0;
   // host shadow of the pointer table
   std::vector<void*> h_ptrs;       // [SLOTS * n]
   std::vector<uint32_t> h_align;   // [n]
@@ -123,6 +129,9 @@ struct gs_plan {
   void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};
   void* last_stream = nullptr;
   void* last_event = nullptr;
+  // launch timer ring (gs_plan_timer_enable)
+  std::vector<void*> timer_ev;  // [2 * slots]: start, stop
+  int timer_next = 0, timer_count = 0;
   gs::PlanArgs args() const;
 };
 
@@ -131,6 +140,8 @@ namespace gs {
 int hip_plan_upload_static(gs_plan* p);
 int hip_plan_release(gs_plan* p);
 int hip_plan_flush(gs_plan* p, void* stream);
+int hip_plan_timer_enable(gs_plan* p, int n_slots);
+int hip_plan_timer_read(gs_plan* p, float* ms_out, int cap);
 int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
              void* stream);
 int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,

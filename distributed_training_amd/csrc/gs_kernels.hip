@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 
@@ -585,6 +586,9 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   GS_TRY_RET(hip_plan_flush(p, stream));
   op.partials = p->d_partials;
+  const int nslots = static_cast<int>(p->timer_ev.size() / 2);
+  const int tk = p->timer_next;
+  if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
   hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(p->grid), dim3(kBlock), 0, s, p->args(), op);
   HIP_RET(hipGetLastError());
   if constexpr (Op::kRed != 0) {
@@ -593,6 +597,11 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
                          (const float*)p->d_partials, p->grid, red_out, accumulate);
       HIP_RET(hipGetLastError());
     }
+  }
+  if (nslots) {
+    HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]), s));
+    p->timer_next = (tk + 1) % nslots;
+    p->timer_count = std::min(p->timer_count + 1, nslots);
   }
   HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), s));
   p->last_stream = stream;
@@ -666,8 +675,45 @@ int hip_plan_upload_static(gs_plan* p) {
   return GS_OK;
 }
 
+int hip_plan_timer_enable(gs_plan* p, int n_slots) {
+  DeviceGuard g(p->device);
+  for (void* ev : p->timer_ev) {
+    (void)hipEventSynchronize(static_cast<hipEvent_t>(ev));
+    (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
+  }
+  p->timer_ev.clear();
+  p->timer_next = p->timer_count = 0;
+  for (int i = 0; i < 2 * n_slots; ++i) {
+    hipEvent_t ev;
+    HIP_RET(hipEventCreate(&ev));
+    p->timer_ev.push_back(ev);
+  }
+  return GS_OK;
+}
+
+int hip_plan_timer_read(gs_plan* p, float* ms_out, int cap) {
+  DeviceGuard g(p->device);
+  const int nslots = static_cast<int>(p->timer_ev.size() / 2);
+  if (nslots == 0) return 0;
+  const int n = std::min(p->timer_count, cap);
+  // oldest recorded pair first
+  const int first = (p->timer_next - p->timer_count + nslots) % nslots;
+  for (int i = 0; i < n; ++i) {
+    const int k = (first + i) % nslots;
+    hipEvent_t a = static_cast<hipEvent_t>(p->timer_ev[2 * k]);
+    hipEvent_t b = static_cast<hipEvent_t>(p->timer_ev[2 * k + 1]);
+    HIP_RET(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIP_RET(hipEventElapsedTime(&ms, a, b));
+    ms_out[i] = ms;
+  }
+  p->timer_count = 0;
+  return n;
+}
+
 int hip_plan_release(gs_plan* p) {
   DeviceGuard g(p->device);
+  (void)hip_plan_timer_enable(p, 0);
   // make sure nothing in flight still reads the tables
   if (p->last_event) (void)hipEventSynchronize(static_cast<hipEvent_t>(p->last_event));
   for (int i = 0; i < 4; ++i) {

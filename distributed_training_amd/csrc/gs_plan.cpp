@@ -1,6 +1,7 @@
 // libgsync: error plumbing, multi-tensor plans and the plan-op entry points,
 // plus the bucket-assignment restatement of torch's Reducer.
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <new>
 
@@ -38,6 +39,28 @@ gs::PlanArgs gs_plan::args() const {
   a.n = n;
   a.n_tasks = static_cast<int32_t>(task_begin.size()) - 1;
   return a;
+}
+
+// Task size (units) of a plan.  Every task is one workgroup's work; the grid
+// holds at most kMaxGrid = 256 CUs x 8 resident workgroups.  Tasks are sized
+// so that the whole plan is ~kTargetTasks tasks: one wave of workgroups,
+// evenly spread over the CUs (no second partial round, no CU with one task
+// more than its neighbours for a long tail), rounded to whole 256-lane
+// iterations and clamped to [kMinTaskUnits, kSegUnits].
+// GS_TASK_UNITS=<n> / GS_TARGET_TASKS=<n> in the environment override (tuning runs).
+int64_t plan_task_units(int64_t total_units) {
+  static const int64_t forced = [] {
+    const char* e = std::getenv("GS_TASK_UNITS");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+  }();
+  static const int64_t target = [] {
+    const char* e = std::getenv("GS_TARGET_TASKS");
+    return e && std::atoll(e) > 0 ? std::atoll(e) : int64_t(kTargetTasks);
+  }();
+  if (forced > 0) return std::max<int64_t>(kUnit, std::min<int64_t>(forced, int64_t(1) << 20));
+  int64_t u = (total_units + target - 1) / target;
+  u = (u + kBlock - 1) / kBlock * kBlock;
+  return std::max<int64_t>(kMinTaskUnits, std::min<int64_t>(kSegUnits, u));
 }
 
 extern "C" {
@@ -79,26 +102,31 @@ int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* nu
   }
   p->flat_numel = rup(cur);
   // segments and tasks
+  int64_t total_units = 0;
+  for (int t = 0; t < n_tensors; ++t) total_units += (numels[t] + kUnit - 1) / kUnit;
+  const int64_t task_units = plan_task_units(total_units);
+  p->task_units = task_units;
   for (int t = 0; t < n_tensors; ++t) {
     const int64_t units = (numels[t] + kUnit - 1) / kUnit;
-    for (int64_t u = 0; u < units; u += kSegUnits) {
+    for (int64_t u = 0; u < units; u += task_units) {
       Seg s{};
       s.unit_begin = u;
       s.tensor = t;
-      s.units = static_cast<int32_t>(std::min<int64_t>(kSegUnits, units - u));
+      s.units = static_cast<int32_t>(std::min<int64_t>(task_units, units - u));
       p->segs.push_back(s);
     }
   }
   p->task_begin.push_back(0);
-  int32_t tu = 0, tc = 0;
+  int64_t tu = 0;
+  int32_t tc = 0;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     Seg& s = p->segs[i];
-    if (tc > 0 && (tu + s.units > kTaskUnits || tc == kMaxSegPerTask)) {
+    if (tc > 0 && (tu + s.units > task_units || tc == kMaxSegPerTask)) {
       p->task_begin.push_back(static_cast<int32_t>(i));
       tu = 0;
       tc = 0;
     }
-    s.task_off = tu;
+    s.task_off = static_cast<int32_t>(tu);
     tu += s.units;
     ++tc;
   }
@@ -135,6 +163,21 @@ int gs_plan_offsets(gs_plan* p, int64_t* out) {
 }
 
 int gs_plan_n_tasks(gs_plan* p) { return p ? static_cast<int>(p->task_begin.size()) - 1 : -1; }
+
+int64_t gs_plan_task_units(gs_plan* p) { return p ? p->task_units : -1; }
+
+int gs_plan_timer_enable(gs_plan* p, int n_slots) {
+  GS_CHECK_ARG(p != nullptr, "gs_plan_timer_enable: NULL plan");
+  GS_CHECK_ARG(n_slots >= 0 && n_slots <= 4096, "gs_plan_timer_enable: n_slots out of [0, 4096]");
+  if (p->kind != GS_DEV_HIP) return fail(GS_EINVAL, "gs_plan_timer_enable: host plans have no launch timer");
+  return hip_plan_timer_enable(p, n_slots);
+}
+
+int gs_plan_timer_read(gs_plan* p, float* ms_out, int cap) {
+  GS_CHECK_ARG(p != nullptr && (cap == 0 || ms_out != nullptr), "gs_plan_timer_read: NULL argument");
+  if (p->kind != GS_DEV_HIP) return fail(GS_EINVAL, "gs_plan_timer_read: host plans have no launch timer");
+  return hip_plan_timer_read(p, ms_out, cap);
+}
 
 int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* /*stream*/) {
   GS_CHECK_ARG(p != nullptr, "gs_plan_set_ptrs: NULL plan");

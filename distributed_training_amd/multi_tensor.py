@@ -69,6 +69,25 @@ class TensorListPlan:
         L.check(L.lib().gs_plan_set_ptrs(self.handle, slot, L.ptr_array(ptrs), None), "gs_plan_set_ptrs")
         self._slot_cache[slot] = ptrs
 
+    @property
+    def n_tasks(self) -> int:
+        return int(L.lib().gs_plan_n_tasks(self.handle))
+
+    @property
+    def task_units(self) -> int:
+        return int(L.lib().gs_plan_task_units(self.handle))
+
+    def timer_enable(self, n_slots: int = 256):
+        """Bracket every launch of this plan with HIP timing events on its
+        launch stream (ring of n_slots); 0 disables."""
+        L.check(L.lib().gs_plan_timer_enable(self.handle, int(n_slots)), "gs_plan_timer_enable")
+
+    def timer_read(self, cap: int = 4096) -> list:
+        """Kernel durations (ms) recorded since the last read, oldest first."""
+        out = (ctypes.c_float * max(1, cap))()
+        n = L.check(L.lib().gs_plan_timer_read(self.handle, out, int(cap)), "gs_plan_timer_read")
+        return [float(out[i]) for i in range(n)]
+
     # ------------------------------------------------------------------ ops
     def pack(self, src_slot, src_dtype, flat: torch.Tensor, scale=1.0, mode=L.GS_SCALE_NONE, stream=None):
         L.check(

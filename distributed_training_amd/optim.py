@@ -40,14 +40,20 @@ class _PlanCache:
 
     def __init__(self):
         self._plans: dict = {}
+        self.timer_slots = 0
 
     def get(self, params):
         key = tuple(id(p) for p in params) + (params[0].device,)
         plan = self._plans.get(key)
         if plan is None:
             plan = TensorListPlan([p.numel() for p in params], params[0].device)
+            if self.timer_slots and plan.kind == L.GS_DEV_HIP:
+                plan.timer_enable(self.timer_slots)
             self._plans[key] = plan
         return plan
+
+    def plans(self):
+        return list(self._plans.values())
 
 
 def _check_dense(p: torch.Tensor, g: torch.Tensor, what: str):
@@ -64,6 +70,18 @@ class _FusedBase(torch.optim.Optimizer):
         self.grad_scale: torch.Tensor | None = None
         self.found_inf: torch.Tensor | None = None
         self._clip_buf: dict = {}
+
+    def enable_kernel_timer(self, n_slots: int = 256):
+        """Time every update-kernel launch with HIP events recorded on its
+        launch stream right around the kernel (bench.py's roofline)."""
+        self._plans.timer_slots = int(n_slots)
+        for plan in self._plans.plans():
+            if plan.kind == L.GS_DEV_HIP:
+                plan.timer_enable(n_slots)
+
+    def kernel_ms(self) -> list:
+        """Update-kernel durations (ms) since the last call, all plans."""
+        return [ms for plan in self._plans.plans() if plan.kind == L.GS_DEV_HIP for ms in plan.timer_read()]
 
     def _skipped_on_host(self) -> bool:
         """Host read of the AMP ``found_inf`` flag, for the cases a device-side

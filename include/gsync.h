@@ -127,6 +127,17 @@ int gs_plan_destroy(gs_plan* p);
 int64_t gs_plan_flat_numel(gs_plan* p);
 int gs_plan_offsets(gs_plan* p, int64_t* out /* [n_tensors] */);
 int gs_plan_n_tasks(gs_plan* p);
+/* units (4 elements) per task of the plan's work decomposition */
+int64_t gs_plan_task_units(gs_plan* p);
+/* launch timer: when enabled (n_slots > 0) every kernel launched through the
+ * plan is bracketed by a pair of timing HIP events recorded on the launch
+ * stream, immediately around the kernel (after any pointer-table upload), in
+ * a ring of n_slots pairs; n_slots = 0 disables and frees them.
+ * gs_plan_timer_read waits for the recorded pairs and writes up to `cap`
+ * durations (ms, oldest first), returning how many it wrote, then clears.
+ * (bench.py's roofline.avg_launch_ms; no torch counterpart.) */
+int gs_plan_timer_enable(gs_plan* p, int n_slots);
+int gs_plan_timer_read(gs_plan* p, float* ms_out, int cap);
 /* register the per-tensor pointers of one slot (uploads on change, ordered on `stream`) */
 int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* stream);
 

@@ -234,3 +234,45 @@ def test_large_sgd_property(cuda_device):
     torch.cuda.synchronize()
     assert np.array_equal(to_np(p), rp)
     assert np.array_equal(to_np(b), rb)
+
+
+def test_resnet50_shaped_sgd_bitwise(cuda_device):
+    """The real ResNet-50 parameter list (161 tensors, 108 of them <= 16 KiB) under the
+    balanced task sizing: every segment boundary / shared task lands bit-exact."""
+    from distributed_training_amd.resnet import MODELS
+
+    sizes = [p.numel() for p in MODELS["resnet50"]().parameters()]
+    ps = rand_list(sizes, torch.float32, cuda_device, seed=1)
+    gs = rand_list(sizes, torch.float32, cuda_device, seed=2, scale=0.01)
+    bs = rand_list(sizes, torch.float32, cuda_device, seed=3, scale=0.01)
+    ref = [O.sgd(to_np(p), to_np(g), to_np(b), 0.1, 0.9, 0.0, 1e-4, False, False, False)
+           for p, g, b in zip(ps, gs, bs)]
+    plan = plan_for(ps, cuda_device)
+    assert plan.n_tasks <= 2048 and plan.task_units % 256 == 0
+    plan.set_ptrs(0, ps)
+    plan.set_ptrs(1, gs)
+    plan.set_ptrs(2, bs)
+    plan.sgd(torch.float32, 0.1, 0.9, 0.0, 1e-4, False, False, False)
+    torch.cuda.synchronize()
+    for (rp, rb), p, b in zip(ref, ps, bs):
+        assert np.array_equal(to_np(p), rp)
+        assert np.array_equal(to_np(b), rb)
+
+
+def test_plan_launch_timer(cuda_device):
+    n = 1 << 22
+    p, g, b = (torch.randn(n, device=cuda_device) for _ in range(3))
+    plan = plan_for([p], cuda_device)
+    plan.set_ptrs(0, [p])
+    plan.set_ptrs(1, [g])
+    plan.set_ptrs(2, [b])
+    assert plan.timer_read() == []  # disabled: nothing recorded
+    plan.timer_enable(4)
+    for _ in range(6):
+        plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
+    ms = plan.timer_read()
+    assert len(ms) == 4 and all(0 < t < 100 for t in ms)  # ring keeps the last 4
+    assert plan.timer_read() == []  # read clears
+    plan.timer_enable(0)
+    plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
+    assert plan.timer_read() == []

@@ -280,3 +280,26 @@ def test_bucketer_mark_unused_packs_zeros():
     assert torch.equal(bufs[0][:20], torch.zeros(20))  # the unused parameter's slot
     L.check(lib.gs_bucketer_finalize(h, None), "finalize")
     L.check(lib.gs_bucketer_destroy(h), "destroy")
+
+
+def test_plan_task_sizing():
+    """Balanced decomposition: ~1920 tasks (one resident wave of <= 2048 workgroups),
+    whole 256-unit iterations, clamped to [256, 16384] units (1 unit = 4 elements)."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.multi_tensor import TensorListPlan
+    from distributed_training_amd.resnet import MODELS
+
+    cpu = torch.device("cpu")
+    small = TensorListPlan([10, 1000], cpu)
+    assert small.task_units == 256 and small.n_tasks == 1
+    for name in ("resnet18", "resnet50", "resnet152"):
+        sizes = [p.numel() for p in MODELS[name]().parameters()]
+        plan = TensorListPlan(sizes, cpu)
+        units = sum((n + 3) // 4 for n in sizes)
+        assert plan.task_units % 256 == 0 and 256 <= plan.task_units <= 16384
+        assert plan.n_tasks <= 2048, (name, plan.n_tasks)
+        assert plan.n_tasks >= units // plan.task_units
+    huge = TensorListPlan([400_000_000], cpu)
+    assert huge.task_units == 16384
+    with pytest.raises(L.GsyncError, match="host plans"):
+        small.timer_enable(4)
