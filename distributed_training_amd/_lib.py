@@ -73,6 +73,7 @@ SIGNATURES = {
     "gs_all_gather": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp]),
     "gs_broadcast": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _vp]),
     "gs_plan_create": (_c_int, [_c_int, _c_int, _c_int, _p_i64, _c_i64, _p_vp]),
+    "gs_plan_create_ex": (_c_int, [_c_int, _c_int, _c_int, _p_i64, _c_i64, _c_i64, _p_vp]),
     "gs_plan_destroy": (_c_int, [_vp]),
     "gs_plan_flat_numel": (_c_i64, [_vp]),
     "gs_plan_offsets": (_c_int, [_vp, _p_i64]),

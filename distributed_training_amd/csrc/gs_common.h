@@ -47,9 +47,9 @@ inline bool is_float_dtype(int dt) { return dt == GS_F32 || dt == GS_BF16 || dt 
 // (small tensors share a task; their descriptors are staged in LDS).
 constexpr int kUnit = 4;
 #ifndef GS_SEG_UNITS
-#define GS_SEG_UNITS 16384
+#define GS_SEG_UNITS 4096
 #endif
-constexpr int kSegUnits = GS_SEG_UNITS;   // max task: 64Ki elements = 256 KiB fp32 per stream
+constexpr int kSegUnits = GS_SEG_UNITS;   // max task: 16Ki elements = 64 KiB fp32 per stream
 constexpr int kMinTaskUnits = 256;        // one unit per lane of a 256-thread workgroup
 #ifndef GS_TARGET_TASKS
 #define GS_TARGET_TASKS 1920

@@ -96,7 +96,7 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #define GS_NT_LOAD 0
 #endif
 #ifndef GS_NT_STORE
-#define GS_NT_STORE 0
+#define GS_NT_STORE 1
 #endif
 #ifndef GS_PACK_ILP
 #define GS_PACK_ILP 4

@@ -42,11 +42,13 @@ gs::PlanArgs gs_plan::args() const {
 }
 
 // Task size (units) of a plan.  Every task is one workgroup's work; the grid
-// holds at most kMaxGrid = 256 CUs x 8 resident workgroups.  Tasks are sized
-// so that the whole plan is ~kTargetTasks tasks: one wave of workgroups,
-// evenly spread over the CUs (no second partial round, no CU with one task
-// more than its neighbours for a long tail), rounded to whole 256-lane
-// iterations and clamped to [kMinTaskUnits, kSegUnits].
+// holds at most kMaxGrid = 256 CUs x 8 resident workgroups.  Plans up to
+// ~1920 x 16 Ki elements are cut into ~kTargetTasks tasks: one wave of
+// workgroups evenly spread over the CUs (no second partial round), rounded to
+// whole 256-lane iterations.  Larger plans keep 16 Ki-element tasks
+// (kSegUnits): the interleaved sweep (profiles/r1d_sweep_tasks_nt.jsonl)
+// puts 64 Ki-element tasks 20-25 % below 8-16 Ki-element ones on pack/unpack
+// of 120 M-element plans, while a second round of tasks costs little there.
 // GS_TASK_UNITS=<n> / GS_TARGET_TASKS=<n> in the environment override (tuning runs).
 int64_t plan_task_units(int64_t total_units) {
   static const int64_t forced = [] {
@@ -71,6 +73,13 @@ int gs_device_count(void) { return hip_device_count(); }
 
 int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* numels,
                    int64_t align_elems, gs_plan** out) {
+  return gs_plan_create_ex(device_kind, device, n_tensors, numels, align_elems, 0, out);
+}
+
+int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t* numels,
+                      int64_t align_elems, int64_t task_units_req, gs_plan** out) {
+  GS_CHECK_ARG(task_units_req >= 0 && task_units_req <= (int64_t(1) << 20),
+               "gs_plan_create_ex: task_units out of [0, 2^20]");
   GS_CHECK_ARG(out != nullptr, "gs_plan_create: out is NULL");
   GS_CHECK_ARG(n_tensors >= 0, "gs_plan_create: n_tensors < 0");
   GS_CHECK_ARG(n_tensors == 0 || numels != nullptr, "gs_plan_create: numels is NULL");
@@ -104,7 +113,8 @@ int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* nu
   // segments and tasks
   int64_t total_units = 0;
   for (int t = 0; t < n_tensors; ++t) total_units += (numels[t] + kUnit - 1) / kUnit;
-  const int64_t task_units = plan_task_units(total_units);
+  const int64_t task_units =
+      task_units_req > 0 ? std::max<int64_t>(kUnit, task_units_req) : plan_task_units(total_units);
   p->task_units = task_units;
   for (int t = 0; t < n_tensors; ++t) {
     const int64_t units = (numels[t] + kUnit - 1) / kUnit;

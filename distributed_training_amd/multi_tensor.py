@@ -18,7 +18,7 @@ from . import _lib as L
 
 
 class TensorListPlan:
-    def __init__(self, numels: Sequence[int], device: torch.device, align: int = 0):
+    def __init__(self, numels: Sequence[int], device: torch.device, align: int = 0, task_units: int = 0):
         self.device = torch.device(device)
         self.kind = L.GS_DEV_HIP if self.device.type == "cuda" else L.GS_DEV_HOST
         self.numels = [int(n) for n in numels]
@@ -30,8 +30,9 @@ class TensorListPlan:
         h = ctypes.c_void_p()
         lib = L.lib()
         L.check(
-            lib.gs_plan_create(self.kind, dev_index, self.n, L.i64_array(self.numels), int(align), ctypes.byref(h)),
-            "gs_plan_create",
+            lib.gs_plan_create_ex(self.kind, dev_index, self.n, L.i64_array(self.numels), int(align),
+                                  int(task_units), ctypes.byref(h)),
+            "gs_plan_create_ex",
         )
         self.handle = h
         self.flat_numel = int(lib.gs_plan_flat_numel(h))

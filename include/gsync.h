@@ -123,6 +123,11 @@ int gs_broadcast(gs_comm* c, const void* send, void* recv, int64_t count, int dt
 #define GS_PLAN_SLOTS 5
 int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* numels,
                    int64_t align_elems, gs_plan** out);
+/* as gs_plan_create, with the work decomposition's task size pinned
+ * (task_units units of 4 elements per workgroup task; 0 = automatic:
+ * ~1920 tasks, one resident wave of workgroups) */
+int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t* numels,
+                      int64_t align_elems, int64_t task_units, gs_plan** out);
 int gs_plan_destroy(gs_plan* p);
 int64_t gs_plan_flat_numel(gs_plan* p);
 int gs_plan_offsets(gs_plan* p, int64_t* out /* [n_tensors] */);
