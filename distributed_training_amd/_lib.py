@@ -36,6 +36,7 @@ GS_BKT_GRAD_VIEW = 2
 GS_BKT_NO_SCALE = 4
 GS_BKT_REDUCE_SCATTER = 8
 GS_BKT_NO_UNPACK = 16
+GS_LAYOUT_NCHW, GS_LAYOUT_NHWC = 0, 1
 
 _TORCH_TO_GS = {
     torch.float32: GS_F32,
@@ -86,6 +87,15 @@ SIGNATURES = {
     "gs_unpack": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_scale": (_c_int, [_vp, _c_int, _c_int, _c_f, _c_int, _vp]),
     "gs_sqnorm": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
+    "gs_rng_state_bytes": (_c_int, []),
+    "gs_rng_draw_u32": (_c_int, [_vp, _c_i64, _c_i64, _vp]),
+    "gs_randperm": (_c_int, [ctypes.c_uint64, _c_i64, _vp]),
+    "gs_distributed_sampler_indices": (_c_int, [_c_i64, _c_int, _c_int, _c_int, ctypes.c_uint64, _c_i64, _c_int,
+                                                _vp, _c_i64, _p_i64]),
+    "gs_crop_flip_params": (_c_int, [_vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_i64,
+                                     _vp]),
+    "gs_image_augment": (_c_int, [_c_int, _c_int, _vp, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                  _vp, _c_i64, _vp, _c_int, _c_int, _vp, _vp]),
     "gs_clip_coef": (_c_int, [_c_int, _vp, _c_f, _c_f, _vp, _vp, _vp]),
     "gs_unscale_check": (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp]),
     "gs_sgd_step": (

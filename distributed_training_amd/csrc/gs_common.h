@@ -136,6 +136,36 @@ struct gs_plan {
 };
 
 namespace gs {
+// ---- input step (gs_data.cpp / gs_data_kernels.hip) ----
+#ifdef __HIPCC__
+#define GS_HD __host__ __device__
+#else
+#define GS_HD
+#endif
+struct ImageAugArgs {
+  const uint8_t* src;     // [n_src, H, W, C] uint8
+  const int64_t* labels;  // [n_src] or NULL
+  int64_t n_src;
+  int H, W, C, pad, out_h, out_w;
+  const int32_t* params;  // [B, 4] = (sample index, flip, top, left)
+  int64_t B;
+  void* out;              // [B, C, out_h, out_w] (NCHW) or [B, out_h, out_w, C] (NHWC)
+  int out_dtype, layout;
+  int64_t* out_labels;    // [B] or NULL
+};
+// Pad(pad, fill 0) -> hflip (of the padded image) -> crop(top, left) -> x/255
+// for one output element (c, y, x) of sample idx; the same expression on the
+// host and the device (IEEE division on both).
+GS_HD inline float aug_pixel(const uint8_t* src, int64_t idx, int H, int W, int C, int pad, int flip,
+                             int top, int left, int c, int y, int x) {
+  const int wp = W + 2 * pad;
+  const int px = flip ? (wp - 1 - (x + left)) : (x + left);
+  const int sy = y + top - pad, sx = px - pad;
+  if (sy < 0 || sy >= H || sx < 0 || sx >= W) return 0.f;
+  return static_cast<float>(src[((idx * H + sy) * W + sx) * C + c]) / 255.f;
+}
+int hip_image_augment(int device, const ImageAugArgs& a, void* stream);
+
 // HIP-side implementations (gs_kernels.hip)
 int hip_plan_upload_static(gs_plan* p);
 int hip_plan_release(gs_plan* p);

@@ -256,6 +256,41 @@ int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
 /* timing of the library's own collective launches (ms of the last iteration, via events) */
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
 
+/* ====================================================================
+ * Input step of the CIFAR configuration
+ * replaces: torch.utils.data.DistributedSampler.__iter__
+ *           (T:utils/data/distributed.py:107-138) and the per-sample
+ *           torchvision 0.15.2 transforms Pad(4) / RandomHorizontalFlip /
+ *           RandomCrop(32) / ToTensor + default_collate, driven by
+ *           DataLoader(num_workers=0) (R:resnet/pytorch_ddp/ddp_train.py:25-48)
+ * ==================================================================== */
+#define GS_LAYOUT_NCHW 0
+#define GS_LAYOUT_NHWC 1
+/* size of torch.get_rng_state() for a CPU generator (MT19937 + caches) */
+int gs_rng_state_bytes(void);
+/* n raw 32-bit MT19937 outputs from torch's serialized CPU generator state,
+ * advancing the state in place exactly as n torch draws would */
+int gs_rng_draw_u32(uint8_t* state, int64_t state_bytes, int64_t n, uint32_t* out);
+/* torch.randperm(n, generator=torch.Generator().manual_seed(seed)) */
+int gs_randperm(uint64_t seed, int64_t n, int64_t* out);
+/* DistributedSampler(n, num_replicas, rank, shuffle, seed, drop_last) with
+ * set_epoch(epoch): this rank's indices (out = NULL: *count only) */
+int gs_distributed_sampler_indices(int64_t n, int num_replicas, int rank, int shuffle, uint64_t seed,
+                                   int64_t epoch, int drop_last, int64_t* out, int64_t cap,
+                                   int64_t* count);
+/* per-sample (index, flip, top, left) for a batch, consuming torch's global
+ * generator state in the reference's order: flip draw (if flip), then the
+ * crop's two draws (unless the padded image equals the crop) per sample */
+int gs_crop_flip_params(const int64_t* indices, int64_t B, int in_h, int in_w, int pad, int out_h,
+                        int out_w, int flip, uint8_t* rng_state, int64_t state_bytes,
+                        int32_t* params /* [B,4] */);
+/* one batch: gather + pad + flip + crop + uint8->float /255 (+ bf16 cast),
+ * labels gathered alongside; device_kind HIP runs one gfx950 kernel on
+ * `stream` (src, labels, params, out in device memory) */
+int gs_image_augment(int device_kind, int device, const uint8_t* src, const int64_t* labels, int64_t n_src,
+                     int H, int W, int C, int pad, int out_h, int out_w, const int32_t* params, int64_t B,
+                     void* out, int out_dtype, int out_layout, int64_t* out_labels, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
