@@ -95,6 +95,75 @@ __global__ void __launch_bounds__(256) augment_kernel(ImageAugArgs a, int64_t to
   }
 }
 
+// One workgroup per sample (grid-stride over samples): the sample's uint8
+// image is staged in LDS with coalesced 16-B loads, then every lane builds
+// 4 consecutive output elements from LDS (32-bit index math only) and writes
+// them with one 16-B / 8-B store.  Used when the image fits the LDS budget
+// (CIFAR: 3 KiB); larger images take augment_kernel (L2-served gathers).
+constexpr int kAugLdsBytes = 48 * 1024;
+
+template <int LAYOUT, int DT>
+__global__ void __launch_bounds__(256) augment_lds_kernel(ImageAugArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_img[];
+  const int img_bytes = a.H * a.W * a.C;
+  const int per = a.C * a.out_h * a.out_w;
+  const int quads = per >> 2;  // per % 4 == 0 (host checks)
+  const int wp = a.W + 2 * a.pad;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const int4 p = reinterpret_cast<const int4*>(a.params)[b];
+    const bool ok = p.x >= 0 && p.x < a.n_src;
+    if (threadIdx.x == 0 && a.out_labels) a.out_labels[b] = (ok && a.labels) ? a.labels[p.x] : 0;
+    __syncthreads();  // previous sample's LDS reads are done
+    if (ok) {
+      const uint8_t* src = a.src + static_cast<int64_t>(p.x) * img_bytes;
+      for (int o = threadIdx.x * 16; o < img_bytes; o += 256 * 16)
+        *reinterpret_cast<uint4*>(s_img + o) = *reinterpret_cast<const uint4*>(src + o);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < quads; q += 256) {
+      const int k0 = q << 2;
+      // (c, y, x) of the quad's first element, then step through the layout's order
+      int c, y, x;
+      if constexpr (LAYOUT == GS_LAYOUT_NCHW) {
+        x = k0 % a.out_w;
+        const int r = k0 / a.out_w;
+        y = r % a.out_h;
+        c = r / a.out_h;
+      } else {
+        c = k0 % a.C;
+        const int pix = k0 / a.C;
+        x = pix % a.out_w;
+        y = pix / a.out_w;
+      }
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int px = p.y ? (wp - 1 - (x + p.w)) : (x + p.w);
+        const int sy = y + p.z - a.pad, sx = px - a.pad;
+        v[i] = (ok && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W)
+                   ? static_cast<float>(s_img[(sy * a.W + sx) * a.C + c]) / 255.f
+                   : 0.f;
+        if constexpr (LAYOUT == GS_LAYOUT_NCHW) {
+          if (++x == a.out_w) { x = 0; if (++y == a.out_h) { y = 0; ++c; } }
+        } else {
+          if (++c == a.C) { c = 0; if (++x == a.out_w) { x = 0; ++y; } }
+        }
+      }
+      const int64_t e = b * per + k0;
+      if constexpr (DT == GS_F32) {
+        gf4 w;
+        w.x = v[0]; w.y = v[1]; w.z = v[2]; w.w = v[3];
+        *reinterpret_cast<gf4*>(static_cast<float*>(a.out) + e) = w;
+      } else {
+        gu2 w;
+        w.x = static_cast<uint32_t>(to_bf16(v[0])) | (static_cast<uint32_t>(to_bf16(v[1])) << 16);
+        w.y = static_cast<uint32_t>(to_bf16(v[2])) | (static_cast<uint32_t>(to_bf16(v[3])) << 16);
+        *reinterpret_cast<gu2*>(static_cast<uint16_t*>(a.out) + e) = w;
+      }
+    }
+  }
+}
+
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -116,6 +185,26 @@ int hip_image_augment(int device, const ImageAugArgs& a, void* stream) {
       (a.B + 255) / 256, std::min<int64_t>((quads + 255) / 256, 8192)));
   const bool vec = (reinterpret_cast<uintptr_t>(a.out) & 15u) == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t img_bytes = static_cast<int64_t>(a.H) * a.W * a.C;
+  const int64_t per = static_cast<int64_t>(a.C) * a.out_h * a.out_w;
+  if (vec && img_bytes <= kAugLdsBytes && img_bytes % 16 == 0 && per % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0) {
+    const int g2 = static_cast<int>(std::min<int64_t>(a.B, 65535));
+    const size_t lds = static_cast<size_t>(img_bytes);
+    if (a.layout == GS_LAYOUT_NCHW) {
+      if (a.out_dtype == GS_F32)
+        hipLaunchKernelGGL((augment_lds_kernel<GS_LAYOUT_NCHW, GS_F32>), dim3(g2), dim3(256), lds, s, a);
+      else
+        hipLaunchKernelGGL((augment_lds_kernel<GS_LAYOUT_NCHW, GS_BF16>), dim3(g2), dim3(256), lds, s, a);
+    } else {
+      if (a.out_dtype == GS_F32)
+        hipLaunchKernelGGL((augment_lds_kernel<GS_LAYOUT_NHWC, GS_F32>), dim3(g2), dim3(256), lds, s, a);
+      else
+        hipLaunchKernelGGL((augment_lds_kernel<GS_LAYOUT_NHWC, GS_BF16>), dim3(g2), dim3(256), lds, s, a);
+    }
+    HIP_RET(hipGetLastError());
+    return GS_OK;
+  }
   if (a.layout == GS_LAYOUT_NCHW) {
     if (a.out_dtype == GS_F32)
       hipLaunchKernelGGL((augment_kernel<GS_LAYOUT_NCHW, GS_F32>), dim3(blocks), dim3(256), 0, s, a, total, vec);

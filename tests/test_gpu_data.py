@@ -69,3 +69,27 @@ def test_full_cifar_shape_epoch(cuda_device):
             assert torch.equal(dev_batches[i][0], x) and torch.equal(dev_batches[i][1], y)
             n += 1
     assert len(dev_batches) == 195 and n == 6
+
+
+@pytest.mark.parametrize("H,W,pad,crop,fmt", [
+    (64, 64, 0, 56, "nchw"),     # LDS path, non-CIFAR geometry
+    (130, 130, 2, 128, "nchw"),  # 50.7 KB image: global-gather path
+    (130, 130, 2, 128, "nhwc"),
+    (9, 7, 1, 5, "nchw"),        # 75 outputs per sample (not a multiple of 4): global-gather path
+    (9, 7, 1, 5, "nhwc"),
+])
+def test_kernel_paths_equal_host(cuda_device, H, W, pad, crop, fmt):
+    g = np.random.default_rng(H * W)
+    imgs = g.integers(0, 256, (37, H, W, 3), dtype=np.uint8)
+    labels = g.integers(0, 10, 37)
+    mf = torch.channels_last if fmt == "nhwc" else torch.contiguous_format
+    tf = D.PadFlipCrop(pad, True, crop)
+    out = {}
+    for dev in ("cpu", cuda_device):
+        ds = D.ImageDataset(imgs, labels, dev)
+        ld = D.DeviceDataLoader(ds, batch_size=6, drop_last=False, transform=tf, memory_format=mf,
+                                sampler=D.DistributedSampler(ds, num_replicas=1, rank=0))
+        torch.manual_seed(4)
+        out[str(dev)] = [(x.cpu(), y.cpu()) for x, y in ld]
+    for (ax, ay), (bx, by) in zip(out["cpu"], out[str(cuda_device)]):
+        assert torch.equal(ax, bx) and torch.equal(ay, by)
