@@ -269,6 +269,8 @@ def main():
             "unit": "images/sec",
             "cores": cb["cores"],
             "kind": "port",
+            "gloo_allreduce_busbw_GBps": cb["gloo_allreduce_busbw_GBps"],
+            "gloo_allreduce_bytes": cb["gloo_allreduce_bytes"],
             "sample": f"torch DDP+gloo {args.model} 224x224, Adam(lr=1e-3*ws), ws=2 x 16 img/rank, "
                       f"1 warmup + 3 timed steps (restates R:resnet/pytorch_ddp/ddp_train.py:79-114 on CPU)",
         }

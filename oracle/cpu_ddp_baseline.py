@@ -60,15 +60,26 @@ def worker(rank, args, q):
             times.append(time.perf_counter() - t0)
         if rank == 0:
             print(f"[cpu_baseline] step {it}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
+    # gloo all-reduce bus bandwidth at the model's fp32 grad size (BASELINE.md CPU plan)
+    nparam = sum(p.numel() for p in model.parameters())
+    buf = torch.ones(nparam)
+    dist.all_reduce(buf)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.ar_iters):
+        dist.all_reduce(buf)
+    dist.barrier()
+    ar_s = (time.perf_counter() - t0) / args.ar_iters
     if rank == 0:
-        q.put(times)
+        q.put((times, ar_s, nparam * 4))
     dist.destroy_process_group()
 
 
-def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29777):
+def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29777, ar_iters=3):
     if cores is None:
         cores = min(16, os.cpu_count() or 1)
-    args = argparse.Namespace(model=model, batch=batch, ws=ws, cores=cores, steps=steps, warmup=warmup, port=port)
+    args = argparse.Namespace(model=model, batch=batch, ws=ws, cores=cores, steps=steps, warmup=warmup, port=port,
+                              ar_iters=ar_iters)
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     procs = [ctx.Process(target=worker, args=(r, args, q)) for r in range(ws)]
@@ -76,9 +87,12 @@ def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29
         p.start()
     for p in procs:
         p.join()
-    times = q.get()
+    times, ar_s, ar_bytes = q.get()
     mean = sum(times) / len(times)
     return {
+        "gloo_allreduce_bytes": ar_bytes,
+        "gloo_allreduce_ms": ar_s * 1e3,
+        "gloo_allreduce_busbw_GBps": ar_bytes / ar_s * 2 * (ws - 1) / ws / 1e9,
         "images_per_sec": ws * batch / mean,
         "step_s": mean,
         "cores": cores,
