@@ -60,8 +60,64 @@ def parse():
     # immediate-mode solutions are what the 5.9k img/s number was measured with
     ap.add_argument("--cudnn-benchmark", type=int, default=0)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU/gloo reference path (rank 0, N=1)")
+    ap.add_argument("--collective-bench", type=int, default=-1,
+                    help="standalone RCCL timing of the step's collectives after the timed region "
+                         "(-1: only when N > 1)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+def collective_bench(ddp, zero, world, iters=10, warmup=3):
+    """The step's collectives alone (after the timed region, every rank): each
+    bucket's all-reduce (DDP) or reduce-scatter + all-gather (ZeRO), back to back
+    on libgsync's comm stream, HIP events around each, after a barrier.
+    busBW = S/t x 2(n-1)/n (all-reduce), S/t x (n-1)/n (RS / AG), S = full buffer
+    bytes, against the xGMI roofline (n-1) x 153 GB/s."""
+    comm = ddp._comm if zero is None else zero._comm
+    if comm is None:
+        return None
+    ops = []
+    if zero is None:
+        for b in ddp._bucketer.buffers:
+            ops.append(("all_reduce", b.numel() * b.element_size(), lambda b=b: comm.all_reduce(b)))
+    else:
+        for g, sh in zip(zero.grad_bufs, zero.grad_shards):
+            if zero.stage == 2:
+                ops.append(("reduce_scatter", g.numel() * g.element_size(),
+                            lambda g=g, sh=sh: comm.reduce_scatter(g, sh)))
+            else:
+                ops.append(("all_reduce", g.numel() * g.element_size(), lambda g=g: comm.all_reduce(g)))
+        for flat, shard in zip(zero.param_flats, zero.param_shards):
+            ops.append(("all_gather", flat.numel() * flat.element_size(),
+                        lambda f=flat, s=shard: comm.all_gather(s, f)))
+    out = []
+    torch.cuda.synchronize()
+    dist.barrier()
+    with torch.cuda.stream(comm.stream):
+        for kind, nbytes, fn in ops:
+            for _ in range(warmup):
+                fn()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+            for a, b in evs:
+                a.record()
+                fn()
+                b.record()
+            out.append((kind, nbytes, evs))
+    torch.cuda.synchronize()
+    rows, tot_ms, tot_bus_bytes = [], 0.0, 0.0
+    peak = (world - 1) * XGMI_LINK_GBPS
+    for kind, nbytes, evs in out:
+        ms = sorted(a.elapsed_time(b) for a, b in evs)[len(evs) // 2]
+        f = 2 * (world - 1) / world if kind == "all_reduce" else (world - 1) / world
+        bus = nbytes / (ms * 1e-3) * f / 1e9
+        rows.append({"op": kind, "bytes": nbytes, "median_ms": ms, "algbw_GBps": nbytes / (ms * 1e-3) / 1e9,
+                     "bus_GBps": bus, "frac": (bus / peak) if peak > 0 else None})
+        tot_ms += ms
+        tot_bus_bytes += nbytes * f
+    agg = tot_bus_bytes / (tot_ms * 1e-3) / 1e9
+    return {"per_op": rows, "ms_per_step": tot_ms, "bus_GBps": agg, "xgmi_peak_GBps": peak,
+            "frac": (agg / peak) if peak > 0 else None,
+            "timing": "HIP events on libgsync's comm stream, median of 10 after 3 warmup, ops back to back"}
 
 
 def main():
@@ -155,6 +211,8 @@ def main():
     comm_ms = []
     if zero is None:
         opt.enable_kernel_timer(args.steps + 4)
+    else:
+        zero.plan.timer_enable(args.steps + 4)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -171,12 +229,19 @@ def main():
     if world > 1 and zero is None:
         comm_ms = ddp.bucket_comm_ms()  # last iteration, per bucket (HIP events on the comm stream)
 
+    coll = None
+    if args.collective_bench == 1 or (args.collective_bench == -1 and world > 1):
+        coll = collective_bench(ddp, zero, world)
+
     if zero is None:
         # update-kernel launches, HIP events recorded by libgsync on the launch stream
         # right around each kernel (the pointer-table upload, if any, stays outside)
         opt_ms = sorted(opt.kernel_ms())
     else:
-        opt_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
+        # the fused shard update alone (plan launch timer); the whole zero.step() window
+        # (norm, clip, update, all-gather) is reported beside it
+        opt_ms = sorted(zero.plan.timer_read())
+        win_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
     opt_ms_avg = sum(opt_ms) / len(opt_ms)
     img_s = world * args.batch * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
@@ -208,7 +273,11 @@ def main():
         bus = sum(bucket_bytes) / (tot_ms * 1e-3) * 2 * (world - 1) / world / 1e9
         peak = (world - 1) * XGMI_LINK_GBPS
         grad_sync.update({"allreduce_ms_per_step": tot_ms, "allreduce_bus_GBps": bus, "xgmi_peak_GBps": peak,
-                          "frac": bus / peak, "per_bucket_ms": comm_ms})
+                          "frac": bus / peak, "per_bucket_ms": comm_ms,
+                          "note": "in-step: HIP events around each bucket collective on the comm stream, "
+                                  "last timed step, includes cross-rank arrival skew under backward"})
+    if coll is not None:
+        grad_sync["standalone"] = coll
     line = {
         "metric": "images/sec (node) ResNet-50 at 1/2/4/8 MI355X; grad-sync bus GB/s",
         "value": img_s,
@@ -241,7 +310,8 @@ def main():
         },
         "roofline": {
             "kernel": (f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
-                       if zero is None else "ZeRO step window: shard Σg² + clip + fused update + all-gather"),
+                       if zero is None else
+                       f"gs ZeRO shard update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> + bf16 param write)"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
@@ -251,11 +321,11 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
             "avg_launch_ms": opt_ms_avg,
             "launches": len(opt_ms),
-            "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
-                       if zero is None else "HIP events around zero.step() on the current stream"),
+            "timing": "libgsync plan launch timer: HIP events recorded on the launch stream around each kernel",
             "median_launch_ms": opt_ms[len(opt_ms) // 2],
         },
         "grad_sync": grad_sync,
+        **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
         "warmup_s": warm_s,
         "has_rebuilt_buckets": log["has_rebuilt_buckets"],
     }
