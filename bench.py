@@ -240,7 +240,9 @@ def main():
     else:
         # the fused shard update alone (plan launch timer); the whole zero.step() window
         # (norm, clip, update, all-gather) is reported beside it
-        opt_ms = sorted(zero.plan.timer_read())
+        from distributed_training_amd import _lib as L
+
+        opt_ms = sorted(zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM))
         win_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
     opt_ms_avg = sum(opt_ms) / len(opt_ms)
     img_s = world * args.batch * args.steps / elapsed

@@ -37,6 +37,7 @@ GS_BKT_NO_SCALE = 4
 GS_BKT_REDUCE_SCATTER = 8
 GS_BKT_NO_UNPACK = 16
 GS_LAYOUT_NCHW, GS_LAYOUT_NHWC = 0, 1
+GS_OP_PACK, GS_OP_UNPACK, GS_OP_SCALE, GS_OP_SQNORM, GS_OP_UNSCALE, GS_OP_SGD, GS_OP_ADAM = 1, 2, 3, 4, 5, 6, 7
 
 _TORCH_TO_GS = {
     torch.float32: GS_F32,
@@ -81,7 +82,7 @@ SIGNATURES = {
     "gs_plan_n_tasks": (_c_int, [_vp]),
     "gs_plan_task_units": (_c_i64, [_vp]),
     "gs_plan_timer_enable": (_c_int, [_vp, _c_int]),
-    "gs_plan_timer_read": (_c_int, [_vp, _p_f, _c_int]),
+    "gs_plan_timer_read": (_c_int, [_vp, _p_f, _p_i32, _c_int]),
     "gs_plan_set_ptrs": (_c_int, [_vp, _c_int, _p_vp, _vp]),
     "gs_pack": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_f, _c_int, _vp]),
     "gs_unpack": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),

@@ -131,6 +131,7 @@ struct gs_plan {
   void* last_event = nullptr;
   // launch timer ring (gs_plan_timer_enable)
   std::vector<void*> timer_ev;  // [2 * slots]: start, stop
+  std::vector<int32_t> timer_kind;  // [slots]: GS_OP_* of the timed launch
   int timer_next = 0, timer_count = 0;
   gs::PlanArgs args() const;
 };
@@ -171,7 +172,7 @@ int hip_plan_upload_static(gs_plan* p);
 int hip_plan_release(gs_plan* p);
 int hip_plan_flush(gs_plan* p, void* stream);
 int hip_plan_timer_enable(gs_plan* p, int n_slots);
-int hip_plan_timer_read(gs_plan* p, float* ms_out, int cap);
+int hip_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap);
 int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
              void* stream);
 int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,

@@ -246,6 +246,7 @@ struct TV {
 //   void load(const TV&, e, Frag&)           issue the unit's loads
 //   void apply(const TV&, e, Frag&, acc)     compute + store (+ reduction)
 //   static constexpr int kRed = 0 (none) | 1 (sum) | 2 (max); float* partials
+//   static constexpr int kKind = GS_OP_* (tags the launch timer's records)
 template <int ILP, class Op>
 __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
                                           const int32_t* s_pref, int ns, int total, float& acc) {
@@ -352,6 +353,7 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
 template <int SD, int FD>
 struct PackOp {
   static constexpr int kRed = 0;
+  static constexpr int kKind = GS_OP_PACK;
   float* partials = nullptr;
   int slot;
   void* flat;
@@ -387,6 +389,7 @@ struct PackOp {
 template <int FD, int DD>
 struct UnpackOp {
   static constexpr int kRed = 1;
+  static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
   bool want_sq;
   const void* flat;
@@ -415,6 +418,7 @@ struct UnpackOp {
 template <int DT>
 struct ScaleOp {
   static constexpr int kRed = 0;
+  static constexpr int kKind = GS_OP_SCALE;
   float* partials = nullptr;
   int slot;
   float s;
@@ -434,6 +438,7 @@ struct ScaleOp {
 template <int DT>
 struct SqnormOp {
   static constexpr int kRed = 1;
+  static constexpr int kKind = GS_OP_SQNORM;
   float* partials = nullptr;
   int slot;
   struct Frag { float x[4]; };
@@ -450,6 +455,7 @@ struct SqnormOp {
 template <int DT>
 struct UnscaleOp {
   static constexpr int kRed = 2;
+  static constexpr int kKind = GS_OP_UNSCALE;
   float* partials = nullptr;
   int slot;
   const float* inv;  // nullable
@@ -477,6 +483,7 @@ struct UnscaleOp {
 template <int GD, int LD>
 struct SgdOp {
   static constexpr int kRed = 0;
+  static constexpr int kKind = GS_OP_SGD;
   float* partials = nullptr;
   SgdHyper h;
   const float* gscale;
@@ -515,6 +522,7 @@ struct SgdOp {
 template <int GD, int LD>
 struct AdamOp {
   static constexpr int kRed = 0;
+  static constexpr int kKind = GS_OP_ADAM;
   float* partials = nullptr;
   AdamHyper h;
   const float* gscale;
@@ -600,6 +608,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   if (nslots) {
     HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]), s));
+    p->timer_kind[tk] = Op::kKind;
     p->timer_next = (tk + 1) % nslots;
     p->timer_count = std::min(p->timer_count + 1, nslots);
   }
@@ -682,6 +691,7 @@ int hip_plan_timer_enable(gs_plan* p, int n_slots) {
     (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
   }
   p->timer_ev.clear();
+  p->timer_kind.assign(n_slots, 0);
   p->timer_next = p->timer_count = 0;
   for (int i = 0; i < 2 * n_slots; ++i) {
     hipEvent_t ev;
@@ -691,7 +701,7 @@ int hip_plan_timer_enable(gs_plan* p, int n_slots) {
   return GS_OK;
 }
 
-int hip_plan_timer_read(gs_plan* p, float* ms_out, int cap) {
+int hip_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap) {
   DeviceGuard g(p->device);
   const int nslots = static_cast<int>(p->timer_ev.size() / 2);
   if (nslots == 0) return 0;
@@ -706,6 +716,7 @@ int hip_plan_timer_read(gs_plan* p, float* ms_out, int cap) {
     float ms = 0.f;
     HIP_RET(hipEventElapsedTime(&ms, a, b));
     ms_out[i] = ms;
+    if (kind_out) kind_out[i] = p->timer_kind[k];
   }
   p->timer_count = 0;
   return n;

@@ -183,10 +183,10 @@ int gs_plan_timer_enable(gs_plan* p, int n_slots) {
   return hip_plan_timer_enable(p, n_slots);
 }
 
-int gs_plan_timer_read(gs_plan* p, float* ms_out, int cap) {
+int gs_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap) {
   GS_CHECK_ARG(p != nullptr && (cap == 0 || ms_out != nullptr), "gs_plan_timer_read: NULL argument");
   if (p->kind != GS_DEV_HIP) return fail(GS_EINVAL, "gs_plan_timer_read: host plans have no launch timer");
-  return hip_plan_timer_read(p, ms_out, cap);
+  return hip_plan_timer_read(p, ms_out, kind_out, cap);
 }
 
 int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* /*stream*/) {

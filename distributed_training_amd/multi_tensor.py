@@ -83,11 +83,13 @@ class TensorListPlan:
         launch stream (ring of n_slots); 0 disables."""
         L.check(L.lib().gs_plan_timer_enable(self.handle, int(n_slots)), "gs_plan_timer_enable")
 
-    def timer_read(self, cap: int = 4096) -> list:
-        """Kernel durations (ms) recorded since the last read, oldest first."""
+    def timer_read(self, cap: int = 4096, kind: int | None = None) -> list:
+        """Kernel durations (ms) recorded since the last read, oldest first
+        (only launches of op `kind` = L.GS_OP_* when given)."""
         out = (ctypes.c_float * max(1, cap))()
-        n = L.check(L.lib().gs_plan_timer_read(self.handle, out, int(cap)), "gs_plan_timer_read")
-        return [float(out[i]) for i in range(n)]
+        kinds = (ctypes.c_int32 * max(1, cap))()
+        n = L.check(L.lib().gs_plan_timer_read(self.handle, out, kinds, int(cap)), "gs_plan_timer_read")
+        return [float(out[i]) for i in range(n) if kind is None or kinds[i] == kind]
 
     # ------------------------------------------------------------------ ops
     def pack(self, src_slot, src_dtype, flat: torch.Tensor, scale=1.0, mode=L.GS_SCALE_NONE, stream=None):

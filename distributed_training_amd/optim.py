@@ -80,8 +80,11 @@ class _FusedBase(torch.optim.Optimizer):
                 plan.timer_enable(n_slots)
 
     def kernel_ms(self) -> list:
-        """Update-kernel durations (ms) since the last call, all plans."""
-        return [ms for plan in self._plans.plans() if plan.kind == L.GS_DEV_HIP for ms in plan.timer_read()]
+        """Update-kernel durations (ms) since the last call, all plans (the
+        Σg² launches of max_grad_norm are left out)."""
+        kind = L.GS_OP_ADAM if isinstance(self, FusedAdam) else L.GS_OP_SGD
+        return [ms for plan in self._plans.plans() if plan.kind == L.GS_DEV_HIP
+                for ms in plan.timer_read(kind=kind)]
 
     def _skipped_on_host(self) -> bool:
         """Host read of the AMP ``found_inf`` flag, for the cases a device-side

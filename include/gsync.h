@@ -139,10 +139,18 @@ int64_t gs_plan_task_units(gs_plan* p);
  * stream, immediately around the kernel (after any pointer-table upload), in
  * a ring of n_slots pairs; n_slots = 0 disables and frees them.
  * gs_plan_timer_read waits for the recorded pairs and writes up to `cap`
- * durations (ms, oldest first), returning how many it wrote, then clears.
+ * durations (ms, oldest first) and, if kind_out is not NULL, the GS_OP_* of
+ * each timed launch; returns how many it wrote, then clears.
  * (bench.py's roofline.avg_launch_ms; no torch counterpart.) */
+#define GS_OP_PACK 1
+#define GS_OP_UNPACK 2
+#define GS_OP_SCALE 3
+#define GS_OP_SQNORM 4
+#define GS_OP_UNSCALE 5
+#define GS_OP_SGD 6
+#define GS_OP_ADAM 7
 int gs_plan_timer_enable(gs_plan* p, int n_slots);
-int gs_plan_timer_read(gs_plan* p, float* ms_out, int cap);
+int gs_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap);
 /* register the per-tensor pointers of one slot (uploads on change, ordered on `stream`) */
 int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* stream);
 

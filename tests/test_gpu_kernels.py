@@ -273,6 +273,13 @@ def test_plan_launch_timer(cuda_device):
     ms = plan.timer_read()
     assert len(ms) == 4 and all(0 < t < 100 for t in ms)  # ring keeps the last 4
     assert plan.timer_read() == []  # read clears
+    from distributed_training_amd import _lib as L
+
+    sq = torch.zeros(1, device=cuda_device)
+    plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
+    plan.sqnorm(1, torch.float32, sq)
+    plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
+    assert len(plan.timer_read(kind=L.GS_OP_SGD)) == 2  # the Σg² launch is tagged apart
     plan.timer_enable(0)
     plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
     assert plan.timer_read() == []
