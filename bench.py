@@ -212,7 +212,7 @@ def main():
     if zero is None:
         opt.enable_kernel_timer(args.steps + 4)
     else:
-        zero.plan.timer_enable(args.steps + 4)
+        zero.plan.timer_enable(4 * args.steps + 8)  # + the Σg² launches of the clip
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
