@@ -80,6 +80,7 @@ __device__ __forceinline__ float round_to(float f) {
 // native 16-B / 8-B vector types.
 typedef float gf4 __attribute__((ext_vector_type(4)));
 typedef uint32_t gu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t gu4 __attribute__((ext_vector_type(4)));
 #define GLOBAL_AS __attribute__((address_space(1)))
 
 template <class T>
@@ -103,6 +104,13 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #endif
 #ifndef GS_OPT_ILP
 #define GS_OPT_ILP 2
+#endif
+// elements per lane-step (4 or 8): 8 gives 16-B accesses to 16-bit streams
+#ifndef GS_PACK_N
+#define GS_PACK_N 4
+#endif
+#ifndef GS_OPT_N
+#define GS_OPT_N 4
 #endif
 // 256-thread workgroups are admitted 8 per CU only while the kernel uses <= 80
 // SGPRs (MI355X_MICROARCH.md, residency); cap the allocation there
@@ -132,60 +140,86 @@ __device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
 #endif
 }
 
-// load 4 consecutive elements [e, e+4) of a tensor with n elements
-template <int DT>
-__device__ __forceinline__ void load4(const void* base, int64_t e, int64_t n, bool vec,
-                                      float (&x)[4]) {
+// load N (4 or 8) consecutive elements [e, e+N) of a tensor with n elements;
+// e is a multiple of N.  fp32: N/4 16-B loads; 16-bit: one 8-B (N=4) or
+// 16-B (N=8) load.  `vec`: the tensor base is 16-B aligned.
+template <int DT, int N>
+__device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bool vec,
+                                      float (&x)[N]) {
+  static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
   if constexpr (DT == GS_F32) {
     const GLOBAL_AS float* p = gptr<float>(base) + e;
-    if (vec && e + 4 <= n) {
-      const gf4 v = vload((const GLOBAL_AS gf4*)p);
-      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    if (vec && e + N <= n) {
+#pragma unroll
+      for (int h = 0; h < N / 4; ++h) {
+        const gf4 v = vload((const GLOBAL_AS gf4*)(p + 4 * h));
+        x[4 * h + 0] = v.x; x[4 * h + 1] = v.y; x[4 * h + 2] = v.z; x[4 * h + 3] = v.w;
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = (e + i < n) ? p[i] : 0.f;
+      for (int i = 0; i < N; ++i) x[i] = (e + i < n) ? p[i] : 0.f;
     }
   } else {
     const GLOBAL_AS uint16_t* p = gptr<uint16_t>(base) + e;
-    if (vec && e + 4 <= n) {
-      const gu2 v = vload((const GLOBAL_AS gu2*)p);
-      x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
-      x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
-      x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
-      x[3] = to_f32<DT>(static_cast<uint16_t>(v.y >> 16));
+    if (vec && e + N <= n) {
+      uint32_t w[N / 2];
+      if constexpr (N == 8) {
+        const gu4 v = vload((const GLOBAL_AS gu4*)p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      } else {
+        const gu2 v = vload((const GLOBAL_AS gu2*)p);
+        w[0] = v.x; w[1] = v.y;
+      }
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k) {
+        x[2 * k] = to_f32<DT>(static_cast<uint16_t>(w[k] & 0xffffu));
+        x[2 * k + 1] = to_f32<DT>(static_cast<uint16_t>(w[k] >> 16));
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = (e + i < n) ? to_f32<DT>(p[i]) : 0.f;
+      for (int i = 0; i < N; ++i) x[i] = (e + i < n) ? to_f32<DT>(p[i]) : 0.f;
     }
   }
 }
 
-template <int DT>
-__device__ __forceinline__ void store4(void* base, int64_t e, int64_t n, bool vec,
-                                       const float (&x)[4]) {
+template <int DT, int N>
+__device__ __forceinline__ void storeN(void* base, int64_t e, int64_t n, bool vec,
+                                       const float (&x)[N]) {
+  static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
   if constexpr (DT == GS_F32) {
     GLOBAL_AS float* p = gptr_w<float>(base) + e;
-    if (vec && e + 4 <= n) {
-      gf4 v;
-      v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
-      vstore((GLOBAL_AS gf4*)p, v);
+    if (vec && e + N <= n) {
+#pragma unroll
+      for (int h = 0; h < N / 4; ++h) {
+        gf4 v;
+        v.x = x[4 * h + 0]; v.y = x[4 * h + 1]; v.z = x[4 * h + 2]; v.w = x[4 * h + 3];
+        vstore((GLOBAL_AS gf4*)(p + 4 * h), v);
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < N; ++i)
         if (e + i < n) p[i] = x[i];
     }
   } else {
     GLOBAL_AS uint16_t* p = gptr_w<uint16_t>(base) + e;
-    if (vec && e + 4 <= n) {
-      gu2 v;
-      v.x = static_cast<uint32_t>(from_f32<DT>(x[0])) |
-            (static_cast<uint32_t>(from_f32<DT>(x[1])) << 16);
-      v.y = static_cast<uint32_t>(from_f32<DT>(x[2])) |
-            (static_cast<uint32_t>(from_f32<DT>(x[3])) << 16);
-      vstore((GLOBAL_AS gu2*)p, v);
+    if (vec && e + N <= n) {
+      uint32_t w[N / 2];
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k)
+        w[k] = static_cast<uint32_t>(from_f32<DT>(x[2 * k])) |
+               (static_cast<uint32_t>(from_f32<DT>(x[2 * k + 1])) << 16);
+      if constexpr (N == 8) {
+        gu4 v;
+        v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+        vstore((GLOBAL_AS gu4*)p, v);
+      } else {
+        gu2 v;
+        v.x = w[0]; v.y = w[1];
+        vstore((GLOBAL_AS gu2*)p, v);
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < N; ++i)
         if (e + i < n) p[i] = from_f32<DT>(x[i]);
     }
   }
@@ -250,33 +284,36 @@ struct TV {
 template <int ILP, class Op>
 __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
                                           const int32_t* s_pref, int ns, int total, float& acc) {
+  // a lane-step covers U consecutive units (U = Op::kN / 4); segments hold an
+  // even number of units (the plan pads), so a step never straddles two
+  constexpr int U = Op::kN / kUnit;
   if (ns == 1) {
     // one (large) tensor segment: descriptor in registers, no per-unit search
     const TV v = s_tv[0];
     const int64_t ub = s_ubeg[0];
-    for (int base = 0; base < total; base += kBlock * ILP) {
+    for (int base = 0; base < total; base += kBlock * ILP * U) {
       typename Op::Frag f[ILP];
 #pragma unroll
       for (int j = 0; j < ILP; ++j) {
-        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
         if (u < total) op.load(v, (ub + u) * kUnit, f[j]);
       }
 #pragma unroll
       for (int j = 0; j < ILP; ++j) {
-        const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
         if (u < total) op.apply(v, (ub + u) * kUnit, f[j], acc);
       }
     }
     return;
   }
   // many small tensors share the task: binary search in the LDS prefix
-  for (int base = 0; base < total; base += kBlock * ILP) {
+  for (int base = 0; base < total; base += kBlock * ILP * U) {
     typename Op::Frag f[ILP];
     int kk[ILP];
     int64_t ee[ILP];
 #pragma unroll
     for (int j = 0; j < ILP; ++j) {
-      const int u = base + j * kBlock + static_cast<int>(threadIdx.x);
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
       kk[j] = -1;
       if (u < total) {
         int lo = 0, hi = ns - 1;
@@ -350,8 +387,9 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
   return static_cast<char*>(flat) + off * (DT == GS_F32 ? 4 : 2);
 }
 
-template <int SD, int FD>
+template <int N, int SD, int FD>
 struct PackOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_PACK;
   float* partials = nullptr;
@@ -360,19 +398,19 @@ struct PackOp {
   bool flat_vec;
   float s;
   int mode;
-  struct Frag { float x[4]; };
+  struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
     const void* src = v.ptr[slot];
     if (src == nullptr) {  // unused parameter (find_unused_parameters): pack zeros
-      f.x[0] = f.x[1] = f.x[2] = f.x[3] = 0.f;
+      for (int i = 0; i < N; ++i) f.x[i] = 0.f;
       return;
     }
-    load4<SD>(src, e, v.numel, v.vec(slot), f.x);
+    loadN<SD, N>(src, e, v.numel, v.vec(slot), f.x);
   }
   __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < N; ++i) {
       float x = f.x[i];
       if (mode == GS_SCALE_MUL) {
         x = x * s;
@@ -382,12 +420,13 @@ struct PackOp {
       }
       f.x[i] = x;
     }
-    store4<FD>(flat_at<FD>(flat, v.off), e, v.numel, flat_vec && (v.off % kUnit) == 0, f.x);
+    storeN<FD, N>(flat_at<FD>(flat, v.off), e, v.numel, flat_vec && (v.off % N) == 0, f.x);
   }
 };
 
-template <int FD, int DD>
+template <int N, int FD, int DD>
 struct UnpackOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 1;
   static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
@@ -395,19 +434,19 @@ struct UnpackOp {
   const void* flat;
   bool flat_vec;
   int slot;
-  struct Frag { float x[4]; };
+  struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    load4<FD>(flat_at<FD>(const_cast<void*>(flat), v.off), e, v.numel,
-              flat_vec && (v.off % kUnit) == 0, f.x);
+    loadN<FD, N>(flat_at<FD>(const_cast<void*>(flat), v.off), e, v.numel,
+              flat_vec && (v.off % N) == 0, f.x);
   }
   __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
     void* dst = v.ptr[slot];
     if (dst == nullptr) return;  // unused parameter: grad left untouched
-    store4<DD>(dst, e, v.numel, v.vec(slot), f.x);
+    storeN<DD, N>(dst, e, v.numel, v.vec(slot), f.x);
     if (want_sq) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < N; ++i) {
         const float r = round_to<DD>(f.x[i]);
         acc = fmaf(r, r, acc);
       }
@@ -415,90 +454,94 @@ struct UnpackOp {
   }
 };
 
-template <int DT>
+template <int N, int DT>
 struct ScaleOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_SCALE;
   float* partials = nullptr;
   int slot;
   float s;
   int mode;
-  struct Frag { float x[4]; };
+  struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
   __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
-    store4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+    for (int i = 0; i < N; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
+    storeN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
 };
 
-template <int DT>
+template <int N, int DT>
 struct SqnormOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 1;
   static constexpr int kKind = GS_OP_SQNORM;
   float* partials = nullptr;
   int slot;
-  struct Frag { float x[4]; };
+  struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
   __device__ void apply(const TV&, int64_t, Frag& f, float& acc) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc = fmaf(f.x[i], f.x[i], acc);
+    for (int i = 0; i < N; ++i) acc = fmaf(f.x[i], f.x[i], acc);
   }
 };
 
-template <int DT>
+template <int N, int DT>
 struct UnscaleOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 2;
   static constexpr int kKind = GS_OP_UNSCALE;
   float* partials = nullptr;
   int slot;
   const float* inv;  // nullable
-  struct Frag { float x[4]; };
+  struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    load4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
   }
   __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < N; ++i)
       if (e + i < v.numel && !isfinite(f.x[i])) acc = 1.f;
     if (inv) {
       const float s = *inv;
       if (s != 1.f) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) f.x[i] = f.x[i] * s;
-        store4<DT>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+        for (int i = 0; i < N; ++i) f.x[i] = f.x[i] * s;
+        storeN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
       }
     }
   }
 };
 
 // SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
-template <int GD, int LD>
+template <int N, int GD, int LD>
 struct SgdOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_SGD;
   float* partials = nullptr;
   SgdHyper h;
   const float* gscale;
   const float* found_inf;
-  struct Frag { float p[4], g[4], b[4]; };
+  struct Frag { float p[N], g[N], b[N]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    load4<GS_F32>(v.ptr[0], e, v.numel, v.vec(0), f.p);
-    load4<GD>(v.ptr[1], e, v.numel, v.vec(1), f.g);
-    if (h.mom != 0.f && !h.first) load4<GS_F32>(v.ptr[2], e, v.numel, v.vec(2), f.b);
+    loadN<GS_F32, N>(v.ptr[0], e, v.numel, v.vec(0), f.p);
+    loadN<GD, N>(v.ptr[1], e, v.numel, v.vec(1), f.g);
+    if (h.mom != 0.f && !h.first) loadN<GS_F32, N>(v.ptr[2], e, v.numel, v.vec(2), f.b);
   }
   __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < N; ++i) {
       float g = f.g[i];
       if (gscale) g = g * gs;                       // clip_grad_norm_ / unscale: grads *= coef
       if (h.maximize) g = -g;
@@ -512,33 +555,34 @@ struct SgdOp {
       }
       f.p[i] = fmaf(-h.lr, d, f.p[i]);              // param.add_(d, alpha=-lr)
     }
-    store4<GS_F32>(v.ptr[0], e, v.numel, v.vec(0), f.p);
-    if (h.mom != 0.f) store4<GS_F32>(v.ptr[2], e, v.numel, v.vec(2), f.b);
-    if constexpr (LD >= 0) store4<LD>(v.ptr[3], e, v.numel, v.vec(3), f.p);
+    storeN<GS_F32, N>(v.ptr[0], e, v.numel, v.vec(0), f.p);
+    if (h.mom != 0.f) storeN<GS_F32, N>(v.ptr[2], e, v.numel, v.vec(2), f.b);
+    if constexpr (LD >= 0) storeN<LD, N>(v.ptr[3], e, v.numel, v.vec(3), f.p);
   }
 };
 
 // Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
-template <int GD, int LD>
+template <int N, int GD, int LD>
 struct AdamOp {
+  static constexpr int kN = N;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_ADAM;
   float* partials = nullptr;
   AdamHyper h;
   const float* gscale;
   const float* found_inf;
-  struct Frag { float p[4], g[4], m[4], v[4]; };
+  struct Frag { float p[N], g[N], m[N], v[N]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
   __device__ void load(const TV& tv, int64_t e, Frag& f) const {
-    load4<GS_F32>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
-    load4<GD>(tv.ptr[1], e, tv.numel, tv.vec(1), f.g);
-    load4<GS_F32>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
-    load4<GS_F32>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
+    loadN<GS_F32, N>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
+    loadN<GD, N>(tv.ptr[1], e, tv.numel, tv.vec(1), f.g);
+    loadN<GS_F32, N>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
+    loadN<GS_F32, N>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
   }
   __device__ void apply(const TV& tv, int64_t e, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < N; ++i) {
       float g = f.g[i];
       if (gscale) g = g * gs;
       if (h.maximize) g = -g;
@@ -553,10 +597,10 @@ struct AdamOp {
       p = fmaf(h.step_size, m / denom, p);                  // addcdiv_(m, denom, -lr/bc1)
       f.p[i] = p; f.m[i] = m; f.v[i] = v;
     }
-    store4<GS_F32>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
-    store4<GS_F32>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
-    store4<GS_F32>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
-    if constexpr (LD >= 0) store4<LD>(tv.ptr[4], e, tv.numel, tv.vec(4), f.p);
+    storeN<GS_F32, N>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
+    storeN<GS_F32, N>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
+    storeN<GS_F32, N>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
+    if constexpr (LD >= 0) storeN<LD, N>(tv.ptr[4], e, tv.numel, tv.vec(4), f.p);
   }
 };
 
@@ -782,7 +826,7 @@ int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, floa
              void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(src_dt, SD, GS_DISPATCH_FLOAT(flat_dt, FD, {
-    PackOp<SD, FD> op;
+    PackOp<GS_PACK_N, SD, FD> op;
     op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s; op.mode = mode;
     return launch<GS_PACK_ILP>(p, op, stream);
   }));
@@ -793,7 +837,7 @@ int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_
                int acc, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
-    UnpackOp<FD, DD> op;
+    UnpackOp<GS_PACK_N, FD, DD> op;
     op.want_sq = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
     return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
   }));
@@ -803,7 +847,7 @@ int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_
 int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    ScaleOp<DT> op;
+    ScaleOp<GS_PACK_N, DT> op;
     op.slot = slot; op.s = s; op.mode = mode;
     return launch<GS_PACK_ILP>(p, op, stream);
   });
@@ -813,7 +857,7 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
 int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    SqnormOp<DT> op;
+    SqnormOp<GS_PACK_N, DT> op;
     op.slot = slot;
     return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
   });
@@ -832,7 +876,7 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
                       void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    UnscaleOp<DT> op;
+    UnscaleOp<GS_PACK_N, DT> op;
     op.slot = slot; op.inv = inv;
     // found_inf accumulates (max) into the caller's flag, as torch's kernel does
     return launch<GS_PACK_ILP>(p, op, stream, found, 1);
@@ -844,7 +888,7 @@ int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, c
             void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    SgdOp<GD, LD> op;
+    SgdOp<GS_OPT_N, GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi;
     return launch<GS_OPT_ILP>(p, op, stream);
   }));
@@ -855,7 +899,7 @@ int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc,
              void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    AdamOp<GD, LD> op;
+    AdamOp<GS_OPT_N, GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi;
     return launch<GS_OPT_ILP>(p, op, stream);
   }));

@@ -113,8 +113,9 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
   // segments and tasks
   int64_t total_units = 0;
   for (int t = 0; t < n_tensors; ++t) total_units += (numels[t] + kUnit - 1) / kUnit;
-  const int64_t task_units =
+  int64_t task_units =
       task_units_req > 0 ? std::max<int64_t>(kUnit, task_units_req) : plan_task_units(total_units);
+  task_units += task_units & 1;  // even (see the segment padding below)
   p->task_units = task_units;
   for (int t = 0; t < n_tensors; ++t) {
     const int64_t units = (numels[t] + kUnit - 1) / kUnit;
@@ -123,6 +124,9 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
       s.unit_begin = u;
       s.tensor = t;
       s.units = static_cast<int32_t>(std::min<int64_t>(task_units, units - u));
+      // even unit counts: an 8-element lane-step (two units) never straddles
+      // segments; the padding unit lies past the tensor's end and is masked
+      s.units += s.units & 1;
       p->segs.push_back(s);
     }
   }

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--tasks", default="0,1024,2048,3072,4096,6144,8192,16384")
-    ap.add_argument("--ops", default="pack,unpack,sgd,adam")
+    ap.add_argument("--ops", default="pack,unpack,sgd,adam,pack16,sgd16")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     from distributed_training_amd.multi_tensor import TensorListPlan
@@ -51,18 +51,33 @@ def main():
         p.timer_enable(args.launches)
         plans[tu] = p
     flat = torch.zeros(plans[sizes[0]].flat_numel, device=dev)
+    flat16 = torch.zeros(plans[sizes[0]].flat_numel, device=dev, dtype=torch.bfloat16)
+    g16 = [x.to(torch.bfloat16) for x in grads]
+    lp16 = [x.to(torch.bfloat16) for x in params]
+    plans16 = {}
+    for tu in sizes:
+        q = TensorListPlan(numels, dev, align=64, task_units=tu)
+        for slot, ts in enumerate((params, g16, bufs, lp16)):
+            q.set_ptrs(slot, ts)
+        q.timer_enable(args.launches)
+        plans16[tu] = q
     ops = {
         "pack": (8, lambda p: p.pack(1, torch.float32, flat, 0.125, 1)),
         "unpack": (8, lambda p: p.unpack(flat, 2, torch.float32)),
         "sgd": (20, lambda p: p.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)),
         "adam": (28, lambda p: p.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5)),
+        # 16-bit streams: fp32 -> bf16 bucket pack (6 B/param); ZeRO-style SGD with bf16 grads
+        # and a bf16 parameter copy (p 8 + g 2 + buf 8 + lowp 2 = 20 B/param)
+        "pack16": (6, lambda p: p.pack(0, torch.float32, flat16, 0.125, 1)),
+        "sgd16": (20, lambda p: p.sgd(torch.bfloat16, 1e-6, 0.9, 0.0, 1e-4, False, False, False,
+                                      lowp_dtype=torch.bfloat16)),
     }
     sel = args.ops.split(",")
     res = {(tu, op): [] for tu in sizes for op in sel}
     for r in range(args.rounds + 1):  # round 0 = warmup
         for op in sel:
             for tu in sizes:
-                p = plans[tu]
+                p = plans16[tu] if op.endswith("16") else plans[tu]
                 for _ in range(args.launches):
                     ops[op][1](p)
                 t = p.timer_read()
