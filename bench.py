@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--engine", default="ddp", choices=["ddp", "zero1", "zero2"],
                     help="ddp = headline (BASELINE configs[1-2]); zero1/zero2 = DeepSpeed-style (configs[3])")
     ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--grad-as-bucket-view", action="store_true",
+                    help="DDP(gradient_as_bucket_view=True): grads alias the buckets, no unpack pass")
     # MIOpen Find (benchmark=1) tunes every conv for minutes on a fresh box; the
     # immediate-mode solutions are what the 5.9k img/s number was measured with
     ap.add_argument("--cudnn-benchmark", type=int, default=0)
@@ -80,6 +82,10 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
     if zero is None:
         for b in ddp._bucketer.buffers:
             ops.append(("all_reduce", b.numel() * b.element_size(), lambda b=b: comm.all_reduce(b)))
+        # the whole gradient as one message: the size-limited ceiling of the same link set
+        whole = torch.zeros(sum(b.numel() for b in ddp._bucketer.buffers), dtype=ddp._bucketer.buffers[0].dtype,
+                            device=ddp._bucketer.buffers[0].device)
+        ops.append(("all_reduce_whole_grad", whole.numel() * whole.element_size(), lambda: comm.all_reduce(whole)))
     else:
         for g, sh in zip(zero.grad_bufs, zero.grad_shards):
             if zero.stage == 2:
@@ -108,12 +114,13 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
     peak = (world - 1) * XGMI_LINK_GBPS
     for kind, nbytes, evs in out:
         ms = sorted(a.elapsed_time(b) for a, b in evs)[len(evs) // 2]
-        f = 2 * (world - 1) / world if kind == "all_reduce" else (world - 1) / world
+        f = 2 * (world - 1) / world if kind.startswith("all_reduce") else (world - 1) / world
         bus = nbytes / (ms * 1e-3) * f / 1e9
         rows.append({"op": kind, "bytes": nbytes, "median_ms": ms, "algbw_GBps": nbytes / (ms * 1e-3) / 1e9,
                      "bus_GBps": bus, "frac": (bus / peak) if peak > 0 else None})
-        tot_ms += ms
-        tot_bus_bytes += nbytes * f
+        if kind != "all_reduce_whole_grad":  # the step's own collectives only
+            tot_ms += ms
+            tot_bus_bytes += nbytes * f
     agg = tot_bus_bytes / (tot_ms * 1e-3) / 1e9
     return {"per_op": rows, "ms_per_step": tot_ms, "bus_GBps": agg, "xgmi_peak_GBps": peak,
             "frac": (agg / peak) if peak > 0 else None,
@@ -147,7 +154,8 @@ def main():
     n_params = sum(p.numel() for p in model.parameters())
     zero = None
     if args.engine == "ddp":
-        ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype)
+        ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
+                                        gradient_as_bucket_view=args.grad_as_bucket_view)
         if args.optimizer == "sgd":
             opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
             bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
@@ -308,6 +316,7 @@ def main():
             "bucket_cap_mb": 25 if args.bucket_cap_mb is None else args.bucket_cap_mb,
             "bucket_dtype": args.bucket_dtype,
             "channels_last": not args.no_channels_last,
+            "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
             "params": n_params,
         },
         "roofline": {
