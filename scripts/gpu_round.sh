@@ -38,6 +38,7 @@ if [ "${PROFILE:-0}" == "1" ]; then
   echo "== rocprofv3 kernel trace + stats (bench)"
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o bench -- python3 -u bench.py --gpus 1 --steps 5 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
   find $OUT/prof_$TAG -name "*stats*"
+  python3 scripts/overlap.py $(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1) $OUT/overlap_$TAG.json > /dev/null || true
 fi
 if [ "${PMC:-0}" == "1" ]; then
   echo "== PMC traffic (separate passes)"
