@@ -66,6 +66,8 @@ SIGNATURES = {
     "gs_comm_create": (_c_int, [_c_int, _c_int, _p_u8, _c_int, _p_vp]),
     "gs_comm_destroy": (_c_int, [_vp]),
     "gs_comm_abort": (_c_int, [_vp]),
+    "gs_comm_set_timeout": (_c_int, [_vp, _c_i64]),
+    "gs_comm_status": (_c_int, [_vp, ctypes.c_char_p, _c_int]),
     "gs_comm_rank": (_c_int, [_vp]),
     "gs_comm_world": (_c_int, [_vp]),
     "gs_comm_stream": (_c_int, [_vp, _p_vp]),

@@ -10,6 +10,7 @@ bootstrap.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -19,8 +20,11 @@ from . import _lib as L
 _REDUCE_OPS = {"sum": L.GS_SUM, "prod": L.GS_PROD, "max": L.GS_MAX, "min": L.GS_MIN, "avg": L.GS_AVG}
 
 
+DEFAULT_TIMEOUT_MS = 600_000  # torch's default process-group timeout (10 min)
+
+
 class Communicator:
-    def __init__(self, process_group=None, device: torch.device | None = None):
+    def __init__(self, process_group=None, device: torch.device | None = None, timeout_ms: int | None = None):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         if device.type != "cuda":
@@ -46,6 +50,26 @@ class Communicator:
         L.check(lib.gs_comm_stream(h, ctypes.byref(s)), "gs_comm_stream")
         self.stream_ptr = s.value
         self.stream = torch.cuda.ExternalStream(self.stream_ptr, device=device)
+        if timeout_ms is None:
+            timeout_ms = int(os.environ.get("GSYNC_TIMEOUT_MS", DEFAULT_TIMEOUT_MS))
+        self.set_timeout(timeout_ms)
+
+    def set_timeout(self, timeout_ms: int):
+        """Watchdog: abort the communicator when a collective is in flight longer
+        than timeout_ms or RCCL reports an asynchronous error (0 disables)."""
+        L.check(L.lib().gs_comm_set_timeout(self.handle, int(timeout_ms)), "gs_comm_set_timeout")
+        self.timeout_ms = int(timeout_ms)
+
+    def status(self):
+        """(aborted, reason) — a host-side flag read, no device synchronisation."""
+        buf = ctypes.create_string_buffer(512)
+        rc = L.check(L.lib().gs_comm_status(self.handle, buf, 512), "gs_comm_status")
+        return bool(rc), buf.value.decode(errors="replace")
+
+    def check(self):
+        aborted, why = self.status()
+        if aborted:
+            raise L.GsyncError(f"libgsync communicator (rank {self.rank}/{self.world}) aborted: {why}")
 
     def _bootstrap_device(self):
         backend = dist.get_backend(self.pg)

@@ -27,6 +27,8 @@ namespace gs {
 ncclComm_t comm_handle(gs_comm* c);
 hipStream_t comm_stream(gs_comm* c);
 int comm_dtype(int dt, ncclDataType_t* out);
+int comm_check_live(gs_comm* c);
+int comm_track(gs_comm* c, hipStream_t stream);
 }  // namespace gs
 
 using namespace gs;
@@ -129,6 +131,7 @@ int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
 }
 
 int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
+  GS_TRY_RET(comm_check_live(b->comm));
   ncclDataType_t dt;
   GS_TRY_RET(comm_dtype(b->bucket_dtype, &dt));
   ncclResult_t r;
@@ -141,7 +144,7 @@ int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
                       comm_handle(b->comm), cs);
   }
   if (r != ncclSuccess) return fail(GS_ERCCL, std::string("bucket collective: ") + ncclGetErrorString(r));
-  return GS_OK;
+  return comm_track(b->comm, cs);
 }
 
 int launch_bucket(gs_bucketer* b, int bi) {

@@ -6,8 +6,23 @@
 // replaces: torch ProcessGroupNCCL (T:include/torch/csrc/distributed/c10d/
 // ProcessGroupNCCL.hpp:849 allreduce, :836 broadcast, :872 _allgather_base,
 // :887-892 reduce_scatter; dedicated ncclStreams_ :1398).
+//
+// Failure detection ("RCCL error checking plus ncclCommAbort on
+// a timeout"; torch's ProcessGroupNCCL watchdog, T:.../ProcessGroupNCCL.hpp:59-68,
+// 156): with a timeout set, every collective enqueued through the
+// communicator records a completion event; a watchdog thread polls the oldest
+// in-flight one and ncclCommGetAsyncError, and aborts the communicator
+// (ncclCommAbort) when a collective has been in flight longer than the
+// timeout or RCCL reports an asynchronous error.  Every later call on the
+// communicator then fails with the reason (gs_comm_status).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+
+#include <atomic>
+#include <chrono>
+#include <deque>
+#include <mutex>
+#include <thread>
 
 #include "gs_common.h"
 
@@ -15,7 +30,19 @@ struct gs_comm {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   int rank = 0, world = 1, device = 0;
-  bool aborted = false;
+  std::atomic<bool> aborted{false};
+  std::string abort_reason;
+  std::mutex mu;  // enqueue vs abort vs the watchdog's bookkeeping
+  // watchdog
+  int64_t timeout_ms = 0;
+  std::thread wd;
+  std::atomic<bool> wd_stop{false};
+  struct Inflight {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t0;
+  };
+  std::deque<Inflight> inflight;
+  std::vector<hipEvent_t> ev_pool;
 };
 
 namespace gs {
@@ -66,12 +93,72 @@ hipStream_t pick(gs_comm* c, void* stream) {
   return stream ? static_cast<hipStream_t>(stream) : c->stream;
 }
 
+// caller holds c->mu
+void abort_locked(gs_comm* c, const std::string& why) {
+  if (c->aborted.load()) return;
+  c->abort_reason = why;
+  c->aborted.store(true);
+  if (c->comm) (void)ncclCommAbort(c->comm);
+}
+
+void watchdog_loop(gs_comm* c) {
+  (void)hipSetDevice(c->device);
+  using clk = std::chrono::steady_clock;
+  while (!c->wd_stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->aborted.load()) continue;
+    ncclResult_t async = ncclSuccess;
+    if (c->comm && ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
+        async != ncclInProgress) {
+      abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+      continue;
+    }
+    while (!c->inflight.empty() && hipEventQuery(c->inflight.front().ev) == hipSuccess) {
+      c->ev_pool.push_back(c->inflight.front().ev);
+      c->inflight.pop_front();
+    }
+    if (!c->inflight.empty() && c->timeout_ms > 0) {
+      const auto age = std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - c->inflight.front().t0);
+      if (age.count() > c->timeout_ms)
+        abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age.count()) +
+                            " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
+    }
+  }
+}
+
 }  // namespace
 
 // used by the bucketer
 ncclComm_t comm_handle(gs_comm* c) { return c->comm; }
 hipStream_t comm_stream(gs_comm* c) { return c->stream; }
 int comm_dtype(int dt, ncclDataType_t* out) { return to_nccl_dtype(dt, out); }
+
+// before enqueueing a collective: fails once the communicator is aborted
+int comm_check_live(gs_comm* c) {
+  if (!c) return fail(GS_EINVAL, "no communicator");
+  if (c->aborted.load()) return fail(GS_ERCCL, "communicator aborted: " + c->abort_reason);
+  return GS_OK;
+}
+
+// after enqueueing a collective on `stream`: hand its completion to the watchdog
+int comm_track(gs_comm* c, hipStream_t stream) {
+  if (c->timeout_ms <= 0) return GS_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipEvent_t ev;
+  if (!c->ev_pool.empty()) {
+    ev = c->ev_pool.back();
+    c->ev_pool.pop_back();
+  } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    return fail(GS_EHIP, "watchdog: event creation failed");
+  }
+  if (hipEventRecord(ev, stream) != hipSuccess) {
+    c->ev_pool.push_back(ev);
+    return fail(GS_EHIP, "watchdog: event record failed");
+  }
+  c->inflight.push_back({ev, std::chrono::steady_clock::now()});
+  return GS_OK;
+}
 
 }  // namespace gs
 
@@ -119,9 +206,15 @@ int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm*
 
 int gs_comm_destroy(gs_comm* c) {
   if (!c) return GS_OK;
+  if (c->wd.joinable()) {
+    c->wd_stop.store(true);
+    c->wd.join();
+  }
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->comm && !c->aborted) (void)ncclCommDestroy(c->comm);
+  if (c->stream && !c->aborted.load()) (void)hipStreamSynchronize(c->stream);
+  for (auto& f : c->inflight) (void)hipEventDestroy(f.ev);
+  for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
+  if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GS_OK;
@@ -129,9 +222,37 @@ int gs_comm_destroy(gs_comm* c) {
 
 int gs_comm_abort(gs_comm* c) {
   GS_CHECK_ARG(c != nullptr, "gs_comm_abort: NULL comm");
-  if (!c->aborted && c->comm) RCCL_RET(ncclCommAbort(c->comm));
-  c->aborted = true;
+  std::lock_guard<std::mutex> lk(c->mu);
+  abort_locked(c, "aborted by the caller (gs_comm_abort)");
   return GS_OK;
+}
+
+int gs_comm_set_timeout(gs_comm* c, int64_t timeout_ms) {
+  GS_CHECK_ARG(c != nullptr && timeout_ms >= 0, "gs_comm_set_timeout: bad argument");
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->timeout_ms = timeout_ms;
+  }
+  if (timeout_ms > 0 && !c->wd.joinable()) c->wd = std::thread(watchdog_loop, c);
+  return GS_OK;
+}
+
+int gs_comm_status(gs_comm* c, char* reason, int cap) {
+  GS_CHECK_ARG(c != nullptr, "gs_comm_status: NULL comm");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->aborted.load()) {
+    ncclResult_t async = ncclSuccess;
+    if (c->comm && ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
+        async != ncclInProgress)
+      abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+  }
+  if (reason && cap > 0) {
+    const std::string& r = c->abort_reason;
+    const size_t n = std::min(r.size(), static_cast<size_t>(cap - 1));
+    std::memcpy(reason, r.data(), n);
+    reason[n] = 0;
+  }
+  return c->aborted.load() ? 1 : 0;
 }
 
 int gs_comm_rank(gs_comm* c) { return c ? c->rank : -1; }
@@ -145,44 +266,48 @@ int gs_comm_stream(gs_comm* c, void** stream_out) {
 
 int gs_allreduce(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
                  void* stream) {
-  GS_CHECK_ARG(c && !c->aborted, "gs_allreduce: no live communicator");
+  GS_CHECK_ARG(c != nullptr, "gs_allreduce: NULL communicator");
+  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   ncclRedOp_t o;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   GS_TRY_RET(to_nccl_op(op, &o));
   RCCL_RET(ncclAllReduce(send, recv, static_cast<size_t>(count), dt, o, c->comm, pick(c, stream)));
-  return GS_OK;
+  return comm_track(c, pick(c, stream));
 }
 
 int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,
                       int op, void* stream) {
-  GS_CHECK_ARG(c && !c->aborted, "gs_reduce_scatter: no live communicator");
+  GS_CHECK_ARG(c != nullptr, "gs_reduce_scatter: NULL communicator");
+  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   ncclRedOp_t o;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   GS_TRY_RET(to_nccl_op(op, &o));
   RCCL_RET(ncclReduceScatter(send, recv, static_cast<size_t>(recv_count), dt, o, c->comm,
                              pick(c, stream)));
-  return GS_OK;
+  return comm_track(c, pick(c, stream));
 }
 
 int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
                   void* stream) {
-  GS_CHECK_ARG(c && !c->aborted, "gs_all_gather: no live communicator");
+  GS_CHECK_ARG(c != nullptr, "gs_all_gather: NULL communicator");
+  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   RCCL_RET(ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, pick(c, stream)));
-  return GS_OK;
+  return comm_track(c, pick(c, stream));
 }
 
 int gs_broadcast(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
                  void* stream) {
-  GS_CHECK_ARG(c && !c->aborted, "gs_broadcast: no live communicator");
+  GS_CHECK_ARG(c != nullptr, "gs_broadcast: NULL communicator");
+  GS_TRY_RET(comm_check_live(c));
   GS_CHECK_ARG(root >= 0 && root < c->world, "gs_broadcast: bad root");
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   RCCL_RET(ncclBroadcast(send, recv, static_cast<size_t>(count), dt, root, c->comm, pick(c, stream)));
-  return GS_OK;
+  return comm_track(c, pick(c, stream));
 }
 
 }  // extern "C"

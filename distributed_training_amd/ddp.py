@@ -379,6 +379,8 @@ class DistributedDataParallel(nn.Module):
         return self.require_forward_param_sync and self.broadcast_buffers and len(self._module_buffers()) != 0
 
     def forward(self, *inputs, **kwargs):
+        if self._comm is not None:
+            self._comm.check()  # watchdog / RCCL async error surfaces here, like ProcessGroupNCCL's
         grad_sync = torch.is_grad_enabled() and self.require_backward_grad_sync
         if grad_sync:
             self._maybe_rebuild_buckets()

@@ -93,6 +93,15 @@ int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm*
 int gs_comm_destroy(gs_comm* c);
 /* ncclCommAbort: for the failure path (timeout / peer death) */
 int gs_comm_abort(gs_comm* c);
+/* failure detection: with timeout_ms > 0 a watchdog thread aborts the
+ * communicator (ncclCommAbort) when a collective enqueued through it has been
+ * in flight longer than timeout_ms, or RCCL reports an asynchronous error;
+ * later calls then fail with GS_ERCCL.  0 disables the timeout.
+ * replaces: ProcessGroupNCCL's watchdog / TORCH_NCCL_ASYNC_ERROR_HANDLING
+ *           (T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp:59-68, :156) */
+int gs_comm_set_timeout(gs_comm* c, int64_t timeout_ms);
+/* 1 if aborted (reason copied into `reason`, NUL-terminated), 0 if live */
+int gs_comm_status(gs_comm* c, char* reason, int cap);
 int gs_comm_rank(gs_comm* c);
 int gs_comm_world(gs_comm* c);
 /* the dedicated collective stream (hipStream_t) */

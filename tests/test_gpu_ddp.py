@@ -238,3 +238,38 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
             ddp.zero_grad(set_to_none=True)
     if mode == "small_buckets":
         assert len(ddp.bucket_indices()) > 3
+
+
+def test_communicator_watchdog_and_abort(cuda_device):
+    """Failure detection: a live communicator with a short watchdog
+    timeout never trips on completing collectives; after an abort every call fails
+    with the reason instead of hanging."""
+    import time
+
+    import torch.distributed as dist
+
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.comm import Communicator
+    from tests._dist_util import free_port
+
+    if not dist.is_initialized():
+        import os
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(free_port())
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    c = Communicator(None, cuda_device, timeout_ms=500)
+    t = torch.ones(1 << 20, device=cuda_device)
+    for _ in range(200):
+        c.all_reduce(t)
+    torch.cuda.synchronize()
+    time.sleep(0.7)  # > timeout: completed collectives must not count as hung
+    assert c.status() == (False, "")
+    c.abort()
+    aborted, why = c.status()
+    assert aborted and "gs_comm_abort" in why
+    with pytest.raises(L.GsyncError, match="aborted"):
+        c.all_reduce(t)
+    with pytest.raises(L.GsyncError, match="aborted"):
+        c.check()
+    c.close()
