@@ -131,7 +131,23 @@ class _OptimizerWrapper:
         self.optim.zero_grad(set_to_none=set_to_none)
 
     def state_dict(self):
-        return self.optim.state_dict()
+        sd = {"optim": self.optim.state_dict()}
+        if self.scaler is not None:
+            sd["scaler"] = self.scaler.state_dict()
+        return sd
+
+    def load_state_dict(self, sd):
+        self.optim.load_state_dict(sd["optim"])
+        if self.scaler is not None and "scaler" in sd:
+            self.scaler.load_state_dict(sd["scaler"])
+
+
+def _unwrap(model):
+    """The user's nn.Module under the booster's wrappers (autocast / cast / DDP)."""
+    m = model
+    while hasattr(m, "module") and isinstance(m.module, nn.Module):
+        m = m.module
+    return m
 
 
 class TorchDDPPlugin(_DPPluginBase):
@@ -175,6 +191,9 @@ class _ZeroOptimizerWrapper:
 
     def state_dict(self):
         return self.zero.state_dict()
+
+    def load_state_dict(self, sd):
+        self.zero.load_state_dict(sd)
 
 
 class _CastInputs(nn.Module):
@@ -226,7 +245,47 @@ class Booster:
 
     def boost(self, model, optimizer=None, criterion=None, dataloader=None, lr_scheduler=None):
         model, optimizer = self.plugin.configure(model, optimizer, self.mixed_precision)
+        self._zero = optimizer.zero if isinstance(optimizer, _ZeroOptimizerWrapper) else None
         return model, optimizer, criterion, dataloader, lr_scheduler
 
     def backward(self, loss, optimizer):
         optimizer.backward(loss)
+
+    # ---- checkpoint I/O (Booster.save_model / load_model / save_optimizer / load_optimizer).
+    # The reference parses -c/--checkpoint but never saves (R:colossal_train.py:40-42); the
+    # layout kept is the model's torchvision-keyed state_dict, unsharded (shard=False):
+    # for LowLevelZero the fp32 master values gathered from every rank's shard.
+    def save_model(self, model, checkpoint: str, shard: bool = False, **kw):
+        if shard:
+            raise NotImplementedError("sharded model checkpoints are not on the reference path")
+        zero = getattr(self, "_zero", None)
+        sd = zero.consolidated_state_dict() if zero is not None else {
+            k: v.detach().cpu() for k, v in _unwrap(model).state_dict().items()}
+        if not dist.is_initialized() or dist.get_rank() == 0:
+            torch.save(sd, checkpoint)
+        if dist.is_initialized():
+            dist.barrier()
+
+    def load_model(self, model, checkpoint: str, strict: bool = True):
+        sd = torch.load(checkpoint, map_location="cpu", weights_only=True)
+        zero = getattr(self, "_zero", None)
+        if zero is not None:
+            zero.load_consolidated_state_dict(sd)
+        else:
+            target = _unwrap(model)
+            target.load_state_dict({k: v.to(target.state_dict()[k].dtype) for k, v in sd.items()}, strict=strict)
+
+    def save_optimizer(self, optimizer, checkpoint: str, shard: bool = False, **kw):
+        """One file per rank for ZeRO (its shard), one file from rank 0 otherwise."""
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        if getattr(self, "_zero", None) is not None:
+            torch.save(optimizer.state_dict(), f"{checkpoint}.rank{rank}")
+        elif rank == 0:
+            torch.save(optimizer.state_dict(), checkpoint)
+        if dist.is_initialized():
+            dist.barrier()
+
+    def load_optimizer(self, optimizer, checkpoint: str):
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        path = f"{checkpoint}.rank{rank}" if getattr(self, "_zero", None) is not None else checkpoint
+        optimizer.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))

@@ -134,6 +134,7 @@ class WarmupLR:
 
     def load_state_dict(self, sd):
         self.last_batch_iteration = sd["last_batch_iteration"]
+        self._set(self.get_lr()[0])
 
 
 class DeepSpeedEngine(nn.Module):
@@ -294,6 +295,72 @@ class DeepSpeedEngine(nn.Module):
 
     def zero_optimization_stage(self):
         return self.zero_stage
+
+    # ---- checkpoints (DeepSpeed's directory layout; the reference never saves,
+    # R:resnet/deepspeed/deepspeed_train.py:252 start_epoch = 0)
+    #   <dir>/<tag>/mp_rank_00_model_states.pt             rank 0: module state_dict (model dtype,
+    #                                                       torchvision keys) + engine counters
+    #   <dir>/<tag>/zero_pp_rank_<r>_mp_rank_00_optim_states.pt   every rank: its ZeRO shard
+    #                                                       (fp32 master + moments)   [ZeRO]
+    #   <dir>/<tag>/optim_states.pt                        rank 0: optimizer state_dict  [no ZeRO]
+    #   <dir>/latest                                        the tag
+    def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True):
+        tag = f"global_step{self.global_steps}" if tag is None else str(tag)
+        path = os.path.join(save_dir, tag)
+        rank = self.global_rank
+        if rank == 0:
+            os.makedirs(path, exist_ok=True)
+        dist.barrier()
+        if rank == 0:
+            torch.save({"module": {k: v.detach().cpu() for k, v in self.module.state_dict().items()},
+                        "global_steps": self.global_steps, "skipped_steps": self.skipped_steps,
+                        "micro_steps": self.micro_steps,
+                        "lr_scheduler": None if self.lr_scheduler is None else self.lr_scheduler.state_dict(),
+                        "client_state": client_state or {}, "dp_world_size": self.world_size,
+                        "zero_stage": self.zero_stage}, os.path.join(path, "mp_rank_00_model_states.pt"))
+        if self._zero is not None:
+            torch.save(self._zero.state_dict(), os.path.join(path, f"zero_pp_rank_{rank}_mp_rank_00_optim_states.pt"))
+        elif rank == 0:
+            torch.save(self.optimizer.state_dict(), os.path.join(path, "optim_states.pt"))
+        dist.barrier()
+        if save_latest and rank == 0:
+            with open(os.path.join(save_dir, "latest"), "w") as f:
+                f.write(tag)
+        dist.barrier()
+        return True
+
+    def load_checkpoint(self, load_dir, tag=None, load_optimizer_states=True, load_lr_scheduler_states=True):
+        if tag is None:
+            latest = os.path.join(load_dir, "latest")
+            if not os.path.exists(latest):
+                return None, None
+            with open(latest) as f:
+                tag = f.read().strip()
+        path = os.path.join(load_dir, str(tag))
+        ms = torch.load(os.path.join(path, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
+        if ms["dp_world_size"] != self.world_size and self._zero is not None:
+            raise RuntimeError(f"checkpoint has {ms['dp_world_size']} ZeRO shards, this job {self.world_size}")
+        with torch.no_grad():
+            self.module.load_state_dict(ms["module"])
+        self.global_steps, self.skipped_steps = ms["global_steps"], ms["skipped_steps"]
+        self.micro_steps = ms.get("micro_steps", 0)
+        if load_lr_scheduler_states and self.lr_scheduler is not None and ms.get("lr_scheduler") is not None:
+            self.lr_scheduler.load_state_dict(ms["lr_scheduler"])
+        if load_optimizer_states:
+            if self._zero is not None:
+                f = os.path.join(path, f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt")
+                self._zero.load_state_dict(torch.load(f, map_location="cpu", weights_only=True))
+            else:
+                self.optimizer.load_state_dict(torch.load(os.path.join(path, "optim_states.pt"),
+                                                          map_location="cpu", weights_only=True))
+        return path, ms.get("client_state", {})
+
+    def consolidated_fp32_state_dict(self):
+        """zero_to_fp32: the full fp32 model state_dict (collective under ZeRO)."""
+        if self._zero is not None:
+            return self._zero.consolidated_state_dict()
+        return {k: v.detach().float().cpu() if v.is_floating_point() else v.detach().cpu()
+                for k, v in self.module.state_dict().items()}
 
 
 def initialize(args=None, model=None, optimizer=None, model_parameters=None, training_data=None, lr_scheduler=None,

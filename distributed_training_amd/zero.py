@@ -313,12 +313,7 @@ class ZeroDataParallel:
                            found_inf=found_inf)
         # re-replicate the updated parameters: in-place all-gather per bucket
         for b, flat in enumerate(self.param_flats):
-            shard = self.param_shards[b]
-            if self._comm is not None:
-                self._comm.all_gather(shard, flat, stream=L.stream_ptr(self.device))
-            else:
-                chunks = list(flat.chunk(self.world))
-                dist.all_gather(chunks, shard.clone(), group=self.pg)
+            self._all_gather_flat(b, flat)
         overflow = False
         if self.scaler is not None:
             overflow = bool(found_inf.item() != 0)  # DeepSpeed reads the overflow flag on the host
@@ -335,11 +330,94 @@ class ZeroDataParallel:
         return self._scratch[3:4]
 
     def state_dict(self):
-        return {"step": self.step_count, "rank": self.rank, "world": self.world,
-                "master": [m.detach().cpu() for m in self.master],
+        """This rank's optimizer shard (fp32 master + states): DeepSpeed's
+        zero_pp_rank_<r>_mp_rank_00_optim_states layout, one file per rank."""
+        return {"step": self.step_count, "rank": self.rank, "world": self.world, "stage": self.stage,
+                "bucket_numel": list(self.bucket_numel), "kind": self.kind,
+                "master": [m.detach().float().cpu().clone() for m in self.master],
                 "exp_avg": [t.cpu() for t in self.state1], "exp_avg_sq": [t.cpu() for t in self.state2],
                 "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
                 "loss_scaler": None if self.scaler is None else self.scaler.state_dict()}
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        """Restore this rank's shard (same world size and bucket layout)."""
+        if sd["world"] != self.world or sd["rank"] != self.rank or list(sd["bucket_numel"]) != self.bucket_numel:
+            raise RuntimeError(f"ZeRO checkpoint shard is for rank {sd['rank']}/{sd['world']} with buckets "
+                               f"{sd['bucket_numel']}; this engine is rank {self.rank}/{self.world} with "
+                               f"{self.bucket_numel}")
+        self.step_count = int(sd["step"])
+        for m, v in zip(self.master, sd["master"]):
+            m.copy_(v.to(m.device, m.dtype))
+        for t, v in zip(self.state1, sd["exp_avg"]):
+            t.copy_(v.to(t.device))
+        for t, v in zip(self.state2, sd["exp_avg_sq"]):
+            t.copy_(v.to(t.device))
+        for g, saved in zip(self.param_groups, sd["param_groups"]):
+            g.update({k: v for k, v in saved.items() if k in g})
+        if self.scaler is not None and sd.get("loss_scaler") is not None:
+            self.scaler.load_state_dict(sd["loss_scaler"])
+        if self.lowp:  # the model copy follows the master
+            for shard, m in zip(self.param_shards, self.master):
+                shard.copy_(m.to(shard.dtype))
+            for b, flat in enumerate(self.param_flats):
+                self._all_gather_flat(b, flat)
+
+    def _all_gather_flat(self, b, flat):
+        shard = flat[self.rank * self.shard_sizes[b]:(self.rank + 1) * self.shard_sizes[b]]
+        if self._comm is not None:
+            self._comm.all_gather(shard, flat, stream=L.stream_ptr(self.device))
+        else:
+            chunks = list(flat.chunk(self.world))
+            dist.all_gather(chunks, shard.clone(), group=self.pg)
+
+    @torch.no_grad()
+    def consolidated_state_dict(self) -> dict:
+        """The full model ``state_dict`` (torchvision keys, module order) with the
+        fp32 master values for the parameters, gathered from every rank's shard
+        (DeepSpeed ``zero_to_fp32`` / ``get_fp32_state_dict_from_zero_checkpoint``;
+        Colossal ``save_model(shard=False)``).  Collective: every rank calls it
+        and every rank gets it.  Buffers are this rank's."""
+        fulls = []
+        for b, m in enumerate(self.master):
+            full = torch.empty(self.bucket_numel[b], dtype=torch.float32, device=self.device)
+            if self._comm is not None:
+                self._comm.all_gather(m.contiguous(), full, stream=L.stream_ptr(self.device))
+            else:
+                dist.all_gather(list(full.chunk(self.world)), m.contiguous(), group=self.pg)
+            fulls.append(full)
+        by_id = {}
+        for i, p in enumerate(self.params):
+            b, off = self.loc[i]
+            by_id[id(p)] = fulls[b].as_strided(p.size(), p.stride(), off)
+        out = {}
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        pn = {names[id(p)]: id(p) for p in self.params}
+        for k, v in self.module.state_dict().items():
+            out[k] = by_id[pn[k]].detach().cpu().clone() if k in pn else v.detach().cpu().clone()
+        return out
+
+    @torch.no_grad()
+    def load_consolidated_state_dict(self, sd: dict):
+        """Inverse of :meth:`consolidated_state_dict`: fp32 values into the master
+        shards and the (low-precision) model, buffers into the module.  No
+        collective: every rank reads the full dict."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        fulls = [torch.zeros(n, dtype=torch.float32, device=self.device) for n in self.bucket_numel]
+        for i, p in enumerate(self.params):
+            b, off = self.loc[i]
+            fulls[b].as_strided(p.size(), p.stride(), off).copy_(sd[names[id(p)]].to(self.device, torch.float32))
+        for b, full in enumerate(fulls):
+            s = self.shard_sizes[b]
+            if self.lowp:
+                self.master[b].copy_(full[self.rank * s:(self.rank + 1) * s])
+            self.param_flats[b].copy_(full.to(self.dtype))
+        param_keys = {names[id(p)] for p in self.params}
+        bufs = {k: v for k, v in sd.items() if k not in param_keys}
+        missing, unexpected = self.module.load_state_dict(bufs, strict=False)
+        if unexpected or set(missing) - param_keys:
+            raise RuntimeError(f"state_dict mismatch: missing {sorted(set(missing) - param_keys)}, "
+                               f"unexpected {unexpected}")
 
     def close(self):
         for h in self._hooks:

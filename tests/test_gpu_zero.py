@@ -172,3 +172,43 @@ def test_deepspeed_shim_gpu_bf16_stage2(cuda_device, rccl_pg):
     torch.cuda.synchronize()
     assert engine.global_steps == 3
     assert all(torch.isfinite(p.float()).all() for p in model.parameters())
+
+
+def test_deepspeed_checkpoint_resume_gpu(cuda_device, rccl_pg, tmp_path):
+    """ZeRO-2 bf16 on the GPU (RCCL ws=1): save after 2 steps, resume a fresh engine,
+    step 3 == the uninterrupted step 3 bit for bit; consolidated fp32 keys = model keys."""
+    sys.path.insert(0, SHIMS)
+    import copy
+
+    import deepspeed
+
+    def build(seed):
+        cfg = copy.deepcopy(DS_CONFIG)
+        cfg["zero_optimization"]["stage"] = 2
+        cfg["bf16"]["enabled"] = True
+        cfg["train_batch_size"] = 4
+        torch.manual_seed(seed)
+        model = _micro()
+        engine, _, _, _ = deepspeed.initialize(model=model, model_parameters=model.parameters(), config=cfg)
+        return engine, model
+
+    def steps(engine, model, its):
+        for it in its:
+            g = torch.Generator(device=cuda_device).manual_seed(it)
+            x = torch.rand(4, 3, 32, 32, device=cuda_device, generator=g).to(torch.bfloat16)
+            y = torch.randint(0, 10, (4,), device=cuda_device, generator=g)
+            engine.backward(nn.CrossEntropyLoss()(model(x).float(), y))
+            engine.step()
+
+    e1, m1 = build(1)
+    steps(e1, m1, [0, 1])
+    e1.save_checkpoint(str(tmp_path))
+    steps(e1, m1, [2])
+    e2, m2 = build(7)
+    e2.load_checkpoint(str(tmp_path))
+    steps(e2, m2, [2])
+    torch.cuda.synchronize()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a, b), n
+    sd = e1.consolidated_fp32_state_dict()
+    assert list(sd) == list(m1.state_dict())
