@@ -226,8 +226,6 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-        if world > 1 and i == args.steps - 1:
-            pass
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
