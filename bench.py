@@ -232,7 +232,7 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    if world > 1 and zero is None:
+    if zero is None:
         comm_ms = ddp.bucket_comm_ms()  # last iteration, per bucket (HIP events on the comm stream)
 
     coll = None
@@ -276,6 +276,8 @@ def main():
         log = {"has_rebuilt_buckets": 0}
         bucket_bytes = [b.numel() * b.element_size() for b in zero.grad_bufs]
     grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
+    if comm_ms:
+        grad_sync["in_step_collective_ms"] = comm_ms
     if world > 1 and comm_ms and min(comm_ms) > 0:
         tot_ms = sum(comm_ms)
         bus = sum(bucket_bytes) / (tot_ms * 1e-3) * 2 * (world - 1) / world / 1e9

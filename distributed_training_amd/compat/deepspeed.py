@@ -11,6 +11,9 @@ Covered surface:
   the config keys of :172-220 (train_batch_size, optimizer Adam/AdamW/SGD,
   WarmupLR, gradient_clipping, bf16 / fp16 (dynamic loss scale), zero_optimization
   stage 0-2 with reduce_bucket_size / allgather_bucket_size / overlap_comm).
+  engine.save_checkpoint / load_checkpoint (DeepSpeed's directory layout) and
+  consolidated_fp32_state_dict (zero_to_fp32), for resume — the reference
+  itself never saves.
 
 Mapping: stage 0 in fp32 -> libgsync DDP (bucketed RCCL all-reduce + fused
 optimizer); stage 0 with bf16/fp16 (DeepSpeed's BF16_Optimizer / FP16
