@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--collective-bench", type=int, default=-1,
                     help="standalone RCCL timing of the step's collectives after the timed region "
                          "(-1: only when N > 1)")
+    ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: N>1 control-flow rehearsal with ranks sharing GPUs (not a measurement)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -137,9 +139,17 @@ def main():
     if world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if args.pg_backend == "gloo":
+        # rehearsal of the N > 1 control flow on a box with fewer GPUs than ranks:
+        # ranks share the devices round-robin and the bucket collectives go through
+        # gloo (RCCL refuses two ranks on one GPU); never the measured configuration
+        dev = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     import distributed_training_amd as D
@@ -229,7 +239,7 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.pg_backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
     if zero is None:
@@ -317,6 +327,8 @@ def main():
             "bucket_dtype": args.bucket_dtype,
             "channels_last": not args.no_channels_last,
             "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
+            **({"rehearsal": "gloo, ranks sharing GPUs: control flow only, not a measurement"}
+               if args.pg_backend == "gloo" else {}),
             "params": n_params,
         },
         "roofline": {
