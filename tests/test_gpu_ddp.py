@@ -77,6 +77,44 @@ def test_ddp_ws1_rccl_grads_and_sgd(cuda_device, rccl_pg):
     assert all(ms >= 0 for ms in ddp.bucket_comm_ms())
 
 
+@pytest.mark.parametrize("model_name", ["resnet50", "resnet152"])
+def test_ddp_full_size_ws1(cuda_device, rccl_pg, model_name):
+    """BASELINE sizes (ResNet-50: 25.6 M params in 5 rebuilt buckets; ResNet-152:
+    60.2 M in 10), bf16 autocast + channels_last as in bench.py: after the
+    rebuild, every averaged grad == the local grad (ws=1 identity through pack ->
+    RCCL -> unpack) and the fused SGD step == the oracle, bit for bit."""
+    from distributed_training_amd import DistributedDataParallel, FusedSGD
+    from distributed_training_amd.resnet import MODELS
+
+    torch.manual_seed(0)
+    model = MODELS[model_name]().to(cuda_device).to(memory_format=torch.channels_last)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model)
+    opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator(device=cuda_device).manual_seed(3)
+    for it in range(2):  # iteration 0: one bucket; iteration 1: rebuilt buckets
+        x = torch.rand(4, 3, 224, 224, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (4,), device=cuda_device, generator=g)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = torch.nn.functional.cross_entropy(ddp(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            assert torch.equal(p.grad, local[i]), f"iter {it} param {i}"
+        if it == 1:
+            ref = [O.sgd(to_np(p).reshape(-1), to_np(p.grad).reshape(-1), None, 0.1, 0.9, 0.0, 1e-4, False, False,
+                         True) for p in params]
+            opt.step()
+            torch.cuda.synchronize()
+            for i, p in enumerate(params):
+                assert np.array_equal(to_np(p).reshape(-1), ref[i][0]), f"param {i}"
+        opt.zero_grad()
+    assert ddp._get_ddp_logging_data()["has_rebuilt_buckets"] == 1
+    assert len(ddp.bucket_indices()) == (5 if model_name == "resnet50" else 10)
+
+
 def test_ddp_ws1_adam_matches_torch_adam(cuda_device, rccl_pg):
     from distributed_training_amd import DistributedDataParallel, FusedAdam
     from distributed_training_amd.resnet import micro_resnet
