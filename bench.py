@@ -88,6 +88,10 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
         whole = torch.zeros(sum(b.numel() for b in ddp._bucketer.buffers), dtype=ddp._bucketer.buffers[0].dtype,
                             device=ddp._bucketer.buffers[0].device)
         ops.append(("all_reduce_whole_grad", whole.numel() * whole.element_size(), lambda: comm.all_reduce(whole)))
+        # message-size curve of the same link set, for the bucket-size choice (bucket_cap_mb)
+        for mb in (1, 4, 16, 64):
+            buf = torch.zeros(mb * 1024 * 1024 // 4, dtype=torch.float32, device=whole.device)
+            ops.append((f"all_reduce_{mb}MiB", buf.numel() * 4, lambda buf=buf: comm.all_reduce(buf)))
     else:
         for g, sh in zip(zero.grad_bufs, zero.grad_shards):
             if zero.stage == 2:
@@ -120,7 +124,7 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
         bus = nbytes / (ms * 1e-3) * f / 1e9
         rows.append({"op": kind, "bytes": nbytes, "median_ms": ms, "algbw_GBps": nbytes / (ms * 1e-3) / 1e9,
                      "bus_GBps": bus, "frac": (bus / peak) if peak > 0 else None})
-        if kind != "all_reduce_whole_grad":  # the step's own collectives only
+        if kind in ("all_reduce", "reduce_scatter", "all_gather"):  # the step's own collectives only
             tot_ms += ms
             tot_bus_bytes += nbytes * f
     agg = tot_bus_bytes / (tot_ms * 1e-3) / 1e9
