@@ -45,5 +45,11 @@ if [ "${PMC:-0}" == "1" ]; then
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 > $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
   python3 scripts/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG resnet50/sgd $OUT/pmc_traffic_$TAG.json
+  for mo in ${PMC_EXTRA:-}; do  # e.g. PMC_EXTRA="resnet50:adam resnet152:sgd"
+    m=${mo%%:*}; o=${mo#*:}
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_${TAG}_${m}_$o -o k -- python3 scripts/sgd_only.py $m 10 $o >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_${TAG}_${m}_$o -o k -- python3 scripts/sgd_only.py $m 10 $o >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+    python3 scripts/pmc_traffic.py $OUT/pmc_fetch_${TAG}_${m}_$o $OUT/pmc_write_${TAG}_${m}_$o $m/$o $OUT/pmc_traffic_$TAG.json
+  done
 fi
 echo "== done"

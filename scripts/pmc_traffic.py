@@ -10,22 +10,26 @@ import os
 import sys
 
 
-def load(d, counter):
+KERNEL = {"sgd": "SgdOp", "adam": "AdamOp"}
+
+
+def load(d, counter, tag="SgdOp"):
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
-                if "SgdOp" not in name:
+                if tag not in name:
                     continue
                 if row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return vals
 
 
-fetch = load(sys.argv[1], "FETCH_SIZE")
-write = load(sys.argv[2], "WRITE_SIZE")
 key, out = sys.argv[3], sys.argv[4]
+tag = KERNEL.get(key.split("/")[-1], "SgdOp")
+fetch = load(sys.argv[1], "FETCH_SIZE", tag)
+write = load(sys.argv[2], "WRITE_SIZE", tag)
 # skip the first launch (cold TLB / first-touch)
 f = fetch[1:] if len(fetch) > 1 else fetch
 w = write[1:] if len(write) > 1 else write
