@@ -105,6 +105,10 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #ifndef GS_OPT_ILP
 #define GS_OPT_ILP 2
 #endif
+// read-only reductions (Σg²) keep more loads in flight per lane
+#ifndef GS_RED_ILP
+#define GS_RED_ILP 4
+#endif
 // elements per lane-step (4 or 8): 8 gives 16-B accesses to 16-bit streams
 #ifndef GS_PACK_N
 #define GS_PACK_N 4
@@ -859,7 +863,7 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
     SqnormOp<GS_PACK_N, DT> op;
     op.slot = slot;
-    return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
+    return launch<GS_RED_ILP>(p, op, stream, sq, acc);
   });
   return GS_OK;
 }

@@ -54,6 +54,7 @@ def main():
     flat16 = torch.zeros(plans[sizes[0]].flat_numel, device=dev, dtype=torch.bfloat16)
     g16 = [x.to(torch.bfloat16) for x in grads]
     lp16 = [x.to(torch.bfloat16) for x in params]
+    sq = torch.zeros(1, device=dev)
     plans16 = {}
     for tu in sizes:
         q = TensorListPlan(numels, dev, align=64, task_units=tu)
@@ -68,6 +69,7 @@ def main():
         "adam": (28, lambda p: p.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5)),
         # 16-bit streams: fp32 -> bf16 bucket pack (6 B/param); ZeRO-style SGD with bf16 grads
         # and a bf16 parameter copy (p 8 + g 2 + buf 8 + lowp 2 = 20 B/param)
+        "sqnorm": (4, lambda p: p.sqnorm(1, torch.float32, sq)),
         "pack16": (6, lambda p: p.pack(0, torch.float32, flat16, 0.125, 1)),
         "sgd16": (20, lambda p: p.sgd(torch.bfloat16, 1e-6, 0.9, 0.0, 1e-4, False, False, False,
                                       lowp_dtype=torch.bfloat16)),
