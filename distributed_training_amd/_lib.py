@@ -88,6 +88,7 @@ SIGNATURES = {
     "gs_plan_set_ptrs": (_c_int, [_vp, _c_int, _p_vp, _vp]),
     "gs_pack": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_f, _c_int, _vp]),
     "gs_unpack": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
+    "gs_unpack_check": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "gs_scale": (_c_int, [_vp, _c_int, _c_int, _c_f, _c_int, _vp]),
     "gs_sqnorm": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_rng_state_bytes": (_c_int, []),
@@ -128,6 +129,7 @@ SIGNATURES = {
     "gs_bucketer_mark_unused": (_c_int, [_vp, _vp, _p_i32, _p_i32]),
     "gs_bucketer_finalize": (_c_int, [_vp, _vp]),
     "gs_bucketer_unpack_bucket": (_c_int, [_vp, _c_int, _vp]),
+    "gs_bucketer_set_found_inf": (_c_int, [_vp, _vp]),
     "gs_bucketer_last_comm_ms": (_c_int, [_vp, _c_int, _p_f]),
 }
 

@@ -29,9 +29,30 @@ class GradScaler:
         self._growth_tracker = None
         self._per_opt = {}
         self._plans = {}
+        self._ddp = None
+        self._ddp_found = None
+        self.fused_checks = 0  # steps whose inf check came from the DDP unpack (no extra pass)
 
     def is_enabled(self):
         return self._enabled
+
+    def fuse_check_into(self, ddp):
+        """Let ``ddp`` (libgsync DistributedDataParallel) compute the non-finite
+        check of the averaged grads inside its bucket unpack (SURVEY.md §8f-2:
+        "fuse it into pack/unpack"): for a libgsync fused optimizer over exactly
+        the DDP parameters, step() then skips its own check pass."""
+        self._ddp = ddp
+        dev = next(iter(ddp.parameters())).device
+        self._ddp_found = torch.zeros(1, dtype=torch.float32, device=dev)
+        ddp.set_found_inf_target(self._ddp_found)
+        self._ddp_param_ids = frozenset(id(p) for p in ddp._params)
+
+    def _ddp_flag_for(self, optimizer):
+        d = self._ddp
+        if d is None or not d._found_inf_valid:
+            return None
+        ids = frozenset(id(p) for g in optimizer.param_groups for p in g["params"] if p.grad is not None)
+        return self._ddp_found if ids == self._ddp_param_ids else None
 
     def _lazy_init(self, dev):
         if self._scale is None:
@@ -95,7 +116,14 @@ class GradScaler:
         fused = hasattr(optimizer, "found_inf") and hasattr(optimizer, "grad_scale")
         if st["stage"] != "unscaled":
             if fused:
-                self._check(optimizer, unscale=False)  # check only; 1/scale folded into the update
+                flag = self._ddp_flag_for(optimizer)
+                if flag is not None:  # the check already ran inside DDP's unpack
+                    st["inv_scale"].copy_(self._scale.reciprocal())
+                    st["found_inf"].copy_(flag)
+                    self._ddp._found_inf_valid = False
+                    self.fused_checks += 1
+                else:
+                    self._check(optimizer, unscale=False)  # check only; 1/scale folded into the update
                 optimizer.grad_scale = st["inv_scale"]
             else:
                 self._check(optimizer, unscale=True)

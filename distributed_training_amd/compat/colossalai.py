@@ -165,6 +165,8 @@ class TorchDDPPlugin(_DPPluginBase):
         if mixed_precision == "fp16":
             wrapped = _AutocastModule(ddp, torch.float16)
             scaler = GradScaler(device=get_current_device())
+            if isinstance(optimizer, FusedAdam):
+                scaler.fuse_check_into(ddp)  # inf check inside the bucket unpack
         elif mixed_precision == "bf16":
             wrapped = _AutocastModule(ddp, torch.bfloat16)
         return wrapped, _OptimizerWrapper(optimizer, scaler)

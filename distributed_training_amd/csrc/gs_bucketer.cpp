@@ -76,6 +76,7 @@ struct gs_bucketer {
   bool prepared = false;
   float* sqnorm = nullptr;
   int sq_count = 0;
+  float* found_inf = nullptr;  // AMP non-finite flag of the averaged grads (fused into unpack)
   void* producer = nullptr;
   hipEvent_t ev_done = nullptr;
   std::mutex mu;
@@ -99,11 +100,22 @@ void plan_set_one(gs_plan* p, int slot, int t, void* ptr) {
   p->dirty = true;
 }
 
+// after the collective: unpack into the grads (with the fused Σg² or the fused
+// non-finite check), or, when the grads ARE the bucket, just the check
 int unpack_one(gs_bucketer* b, Bucket& bk, void* stream, int accumulate_sq) {
   float* sq = b->sqnorm;
-  const int acc = (b->sq_count > 0 || accumulate_sq) ? 1 : 0;
-  GS_TRY_RET(gs_unpack(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, sq, acc, stream));
-  if (sq) ++b->sq_count;
+  if (b->do_unpack()) {
+    if (b->found_inf && !sq) {
+      GS_TRY_RET(gs_unpack_check(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, b->found_inf, stream));
+    } else {
+      const int acc = (b->sq_count > 0 || accumulate_sq) ? 1 : 0;
+      GS_TRY_RET(gs_unpack(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, sq, acc, stream));
+      if (sq) ++b->sq_count;
+      if (b->found_inf) GS_TRY_RET(gs_unscale_check(bk.flat, 0, b->bucket_dtype, nullptr, b->found_inf, stream));
+    }
+  } else if (b->found_inf) {
+    GS_TRY_RET(gs_unscale_check(bk.flat, 0, b->bucket_dtype, nullptr, b->found_inf, stream));
+  }
   bk.unpacked = true;
   return GS_OK;
 }
@@ -161,7 +173,7 @@ int launch_bucket(gs_bucketer* b, int bi) {
     GS_TRY_RET(launch_collective(b, bk, cs));
     HIPB_RET(hipEventRecord(bk.ev_t1, cs));
     bk.timed = true;
-    if (b->do_unpack()) GS_TRY_RET(unpack_one(b, bk, cs, 0));
+    if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
   } else {
     GS_TRY_RET(pack_one(b, bk, b->producer));
   }
@@ -382,11 +394,20 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
     hipStream_t cs = comm_stream(b->comm);
     HIPB_RET(hipEventRecord(b->ev_done, cs));
     HIPB_RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), b->ev_done, 0));
-  } else if (b->do_unpack()) {
+  } else if (b->do_unpack() || b->found_inf) {
     for (Bucket& bk : b->buckets)
       if (!bk.unpacked) GS_TRY_RET(unpack_one(b, bk, stream, 0));
   }
   b->prepared = false;
+  return GS_OK;
+}
+
+int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_set_found_inf: NULL bucketer");
+  GS_CHECK_ARG(!(b->flags & (GS_BKT_REDUCE_SCATTER | GS_BKT_NO_UNPACK)) || found_inf == nullptr,
+               "gs_bucketer_set_found_inf: sharded (ZeRO) buckets check their shard in the optimizer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  b->found_inf = found_inf;
   return GS_OK;
 }
 

@@ -177,6 +177,8 @@ int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, floa
              void* stream);
 int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
                int acc, void* stream);
+int hip_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found,
+                     void* stream);
 int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream);
 int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream);
 int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm,
@@ -195,6 +197,7 @@ int hip_stream_wait(void* waiter, void* signaler);
 int host_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode);
 int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
                 int acc);
+int host_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found);
 int host_scale(gs_plan* p, int slot, int dt, float s, int mode);
 int host_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc);
 int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm);

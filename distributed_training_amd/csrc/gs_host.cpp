@@ -102,6 +102,25 @@ int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst
   return GS_OK;
 }
 
+int host_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found) {
+  GS_TRY_RET(check_float(flat_dt));
+  GS_TRY_RET(check_float(dst_dt));
+  const int fsz = dtype_size(flat_dt);
+  float f = found[0];
+  for (int t = 0; t < p->n; ++t) {
+    const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
+    void* dst = slot(p, dst_slot, t);
+    if (dst == nullptr) continue;
+    for (int64_t i = 0; i < p->numel[t]; ++i) {
+      const float v = ld(src, flat_dt, i);
+      st(dst, dst_dt, i, v);
+      if (!std::isfinite(round_to(dst_dt, v))) f = 1.f;
+    }
+  }
+  found[0] = f;
+  return GS_OK;
+}
+
 int host_scale(gs_plan* p, int s_, int dt, float s, int mode) {
   GS_TRY_RET(check_float(dt));
   for (int t = 0; t < p->n; ++t) {

@@ -428,13 +428,15 @@ struct PackOp {
   }
 };
 
-template <int N, int FD, int DD>
+// RED = 1: Σ dst² of the written values (fused grad-norm); RED = 2: non-finite
+// flag of the written values (fused AMP inf check, max-combined into the flag)
+template <int N, int FD, int DD, int RED = 1>
 struct UnpackOp {
   static constexpr int kN = N;
-  static constexpr int kRed = 1;
+  static constexpr int kRed = RED;
   static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
-  bool want_sq;
+  bool want_red;
   const void* flat;
   bool flat_vec;
   int slot;
@@ -448,11 +450,12 @@ struct UnpackOp {
     void* dst = v.ptr[slot];
     if (dst == nullptr) return;  // unused parameter: grad left untouched
     storeN<DD, N>(dst, e, v.numel, v.vec(slot), f.x);
-    if (want_sq) {
+    if (want_red) {
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         const float r = round_to<DD>(f.x[i]);
-        acc = fmaf(r, r, acc);
+        if constexpr (RED == 1) acc = fmaf(r, r, acc);
+        else if (e + i < v.numel && !isfinite(r)) acc = 1.f;
       }
     }
   }
@@ -841,9 +844,21 @@ int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_
                int acc, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
-    UnpackOp<GS_PACK_N, FD, DD> op;
-    op.want_sq = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
+    UnpackOp<GS_PACK_N, FD, DD, 1> op;
+    op.want_red = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
     return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
+  }));
+  return GS_OK;
+}
+
+int hip_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found,
+                     void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
+    UnpackOp<GS_PACK_N, FD, DD, 2> op;
+    op.want_red = true; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
+    // the flag accumulates (max), as torch's non-finite check does
+    return launch<GS_PACK_ILP>(p, op, stream, found, 1);
   }));
   return GS_OK;
 }

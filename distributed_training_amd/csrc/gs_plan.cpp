@@ -233,6 +233,16 @@ int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int ds
   return hip_unpack(p, flat, flat_dtype, dst_slot, dst_dtype, sqnorm_dev, accumulate, stream);
 }
 
+int gs_unpack_check(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
+                    float* found_inf, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(dst_slot);
+  GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_unpack_check: NULL flat buffer");
+  GS_CHECK_ARG(found_inf != nullptr, "gs_unpack_check: NULL found_inf");
+  if (p->kind == GS_DEV_HOST) return host_unpack_check(p, flat, flat_dtype, dst_slot, dst_dtype, found_inf);
+  return hip_unpack_check(p, flat, flat_dtype, dst_slot, dst_dtype, found_inf, stream);
+}
+
 int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* stream) {
   PLAN_OK(p);
   SLOT_OK(slot);

@@ -239,6 +239,8 @@ class DistributedDataParallel(nn.Module):
         self._comm_hook: tuple[Any, Callable] | None = None
         self._buffers_plan = None
         self._sqnorm_target: torch.Tensor | None = None
+        self._found_inf_target: torch.Tensor | None = None
+        self._found_inf_valid = False
 
         if init_sync:
             self._verify_param_shape_across_processes()
@@ -279,7 +281,11 @@ class DistributedDataParallel(nn.Module):
         old = getattr(self, "_bucketer", None)
         if old is not None:
             old.close()
-        return _Bucketer(self, buckets, self._flags())
+        b = _Bucketer(self, buckets, self._flags())
+        t = getattr(self, "_found_inf_target", None)
+        if t is not None:
+            L.check(L.lib().gs_bucketer_set_found_inf(b.handle, t.data_ptr()), "gs_bucketer_set_found_inf")
+        return b
 
     def _verify_param_shape_across_processes(self):
         if self.world_size == 1:
@@ -396,6 +402,7 @@ class DistributedDataParallel(nn.Module):
             self._prepare_for_backward()
         else:
             self.require_forward_param_sync = False
+            self._found_inf_valid = False  # grads will change without a synchronising unpack
         return output
 
     def _prepare_for_backward(self):
@@ -404,6 +411,9 @@ class DistributedDataParallel(nn.Module):
                 "Expected to have finished reduction in the prior iteration before starting a new one. "
                 "This error indicates that your module has parameters that were not used in producing loss.")
         sq = self._sqnorm_target
+        if self._found_inf_target is not None:
+            self._found_inf_target.zero_()  # on the producer stream, before any bucket is launched
+        self._found_inf_valid = False
         L.check(L.lib().gs_bucketer_prepare(self._bucketer.handle, None if sq is None else sq.data_ptr()),
                 "gs_bucketer_prepare")
         self._in_backward = True
@@ -482,6 +492,7 @@ class DistributedDataParallel(nn.Module):
                     b.buffers[bi].copy_(res.reshape(-1)[: b.buffers[bi].numel()])
         self._pending = {}
         L.check(L.lib().gs_bucketer_finalize(b.handle, self._stream), "gs_bucketer_finalize")
+        self._found_inf_valid = self._found_inf_target is not None
         if self.gradient_as_bucket_view:
             for i, p in enumerate(self._params):
                 if p.grad is not None:
@@ -537,6 +548,18 @@ class DistributedDataParallel(nn.Module):
             raise TypeError("Communication hook must be callable.")
         self._comm_hook = (state, hook)
         self._bucketer = self._make_bucketer(self._bucketer.buckets)
+
+    def set_found_inf_target(self, t: torch.Tensor | None):
+        """Fuse GradScaler's non-finite check of the averaged grads into the
+        bucket unpack (fp32 1-element device tensor, zeroed by every
+        synchronising backward; ``_found_inf_valid`` tells whether the last
+        backward filled it)."""
+        if t is not None and (t.numel() != 1 or t.dtype != torch.float32 or t.device != self.device):
+            raise ValueError("found_inf target must be a 1-element float32 tensor on the DDP device")
+        self._found_inf_target = t
+        self._found_inf_valid = False
+        L.check(L.lib().gs_bucketer_set_found_inf(self._bucketer.handle, None if t is None else t.data_ptr()),
+                "gs_bucketer_set_found_inf")
 
     def set_grad_sqnorm_target(self, t: torch.Tensor | None):
         """Fuse Σg² of the averaged grads into the unpack (fp32 1-element tensor)."""

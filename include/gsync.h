@@ -175,6 +175,12 @@ int gs_pack(gs_plan* p, int src_slot, int src_dtype, void* flat, int flat_dtype,
  *           T:_utils.py:578 _unflatten_dense_tensors */
 int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
               float* sqnorm_dev, int accumulate, void* stream);
+/* unflatten + cast with the AMP non-finite check of the written grads fused:
+ * found_inf[0] = max(found_inf[0], any dst non-finite ? 1 : 0)
+ * replaces: copy_bucket_to_grad + GradScaler's _amp_foreach_non_finite_check_and_unscale_
+ *           check pass (T:amp/grad_scaler.py:280) over the same grads */
+int gs_unpack_check(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
+                    float* found_inf, void* stream);
 /* in-place x = x (*|/) s on one slot (view-mode bucket_view.div_(div_factor)) */
 int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* stream);
 /* Σ x² over all tensors of one slot into sqnorm_dev[0] (fp32, deterministic order)
@@ -269,6 +275,11 @@ int gs_bucketer_mark_unused(gs_bucketer* b, void* stream, int32_t* ready_out, in
  * the collectives (Reducer::finalize_backward). */
 int gs_bucketer_finalize(gs_bucketer* b, void* stream);
 /* unpack one bucket (external-collective mode: after the caller's collective) */
+/* AMP: fuse the non-finite check of the averaged grads into each bucket's
+ * unpack (found_inf[0] = max(found_inf[0], non-finite ? 1 : 0); the caller
+ * zeroes it before backward); NULL disables.  Replaces the check pass of
+ * GradScaler._unscale_grads_ (T:amp/grad_scaler.py:280) for these grads. */
+int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf);
 int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
 /* timing of the library's own collective launches (ms of the last iteration, via events) */
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
