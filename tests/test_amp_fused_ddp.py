@@ -68,19 +68,36 @@ def test_fused_inf_check_gpu_ws1(cuda_device):
     and it is set exactly on the poisoned iteration; the scaler then backs off."""
     import torch.distributed as dist
 
+    from tests._dist_util import free_port, init_pg
+
+    created = not dist.is_initialized()
+    if created:
+        init_pg("nccl", 0, 1, free_port())
+    try:
+        _gpu_body(cuda_device)
+    finally:
+        if created:
+            from distributed_training_amd.comm import destroy_communicators
+
+            destroy_communicators()
+            dist.destroy_process_group()
+
+
+def _gpu_body(cuda_device):
     import distributed_training_amd as D
     from distributed_training_amd.amp import GradScaler
     from distributed_training_amd.multi_tensor import TensorListPlan
-    from tests._dist_util import free_port, init_pg
 
-    if not dist.is_initialized():
-        init_pg("nccl", 0, 1, free_port())
     dev = cuda_device
     torch.manual_seed(0)
     model = _micro().to(dev)
     state = {"it": 0}
-    next(model.parameters()).register_post_accumulate_grad_hook(
-        lambda p: p.grad.view(-1)[1].fill_(float("inf")) if state["it"] == 2 else None)
+
+    def poison(p):
+        if state["it"] == 2:
+            p.grad.view(-1)[1] = float("inf")
+
+    next(model.parameters()).register_post_accumulate_grad_hook(poison)
     ddp = D.DistributedDataParallel(model)
     opt = D.FusedAdam(ddp.parameters(), lr=1e-3)
     scaler = GradScaler("cuda", init_scale=2.0 ** 8, growth_interval=2)

@@ -31,6 +31,9 @@ def to_np(t):
 
 @pytest.fixture(scope="module")
 def rccl_pg(cuda_device):
+    if dist.is_initialized():  # another module's group is still up
+        yield
+        return
     init_pg("nccl", 0, 1, free_port())
     yield
     from distributed_training_amd.comm import destroy_communicators
