@@ -57,14 +57,15 @@ constexpr int kMinTaskUnits = 256;        // one unit per lane of a 256-thread w
 constexpr int kTargetTasks = GS_TARGET_TASKS;  // < kMaxGrid: ragged tensor ends add tasks
 constexpr int kMaxSegPerTask = 64;
 constexpr int kBlock = 256;         // 4 waves of 64
-constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups
+constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups (default grid cap)
+constexpr int kGridLimit = 65536;   // hard cap (partials buffer); GS_MAX_GRID env for tuning
 
 struct Seg {
-  int64_t unit_begin;  // first unit inside the tensor
+  int64_t unit_begin;  // first unit inside the tensor (interleaved part: the part index)
   int32_t tensor;
-  int32_t units;
+  int32_t units;       // (interleaved part: the tensor's units)
   int32_t task_off;    // unit offset of this segment inside its task
-  int32_t pad;
+  int32_t pad;         // 0 = contiguous segment; M > 0 = one of M interleaved parts
 };
 static_assert(sizeof(Seg) == 24, "Seg layout");
 
@@ -123,7 +124,7 @@ struct gs_plan {
   // device side (HIP plans only)
   void* d_static = nullptr;  // segs | task_begin | numel | off
   void* d_table = nullptr;   // ptrs | align
-  float* d_partials = nullptr;  // [kMaxGrid]
+  float* d_partials = nullptr;  // [kGridLimit]
   void* pinned = nullptr;       // staging ring for table uploads
   int ring = 0;
   void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};

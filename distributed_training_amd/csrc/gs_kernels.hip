@@ -336,6 +336,38 @@ __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const in
   }
 }
 
+// part `part` of `parts` of one tensor of `total` units: lane-step chunks of
+// C = kBlock * ILP * U units, chunk c taken by part c % parts
+template <int ILP, class Op>
+__device__ __forceinline__ void run_interleaved(const Op& op, const TV& v, int part, int parts, int total,
+                                                float& acc) {
+  constexpr int U = Op::kN / kUnit;
+  constexpr int C = kBlock * ILP * U;
+  for (int base = part * C; base < total; base += parts * C) {
+    typename Op::Frag f[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+      if (u < total) op.load(v, static_cast<int64_t>(u) * kUnit, f[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+      if (u < total) op.apply(v, static_cast<int64_t>(u) * kUnit, f[j], acc);
+    }
+  }
+}
+
+// The plan tables are read-only for the whole launch: reading them through
+// the constant address space lets the uniform descriptor loads of a
+// single-segment task go to the scalar unit (s_load), with no LDS round trip
+// and no barrier before the first data load.
+#define CONST_AS __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ T cload(const T* p, int64_t i) {
+  return ((const CONST_AS T*)(p))[i];
+}
+
 template <int ILP, class Op>
 __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op op) {
   __shared__ TV s_tv[kMaxSegPerTask];
@@ -344,8 +376,26 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
   float acc = 0.f;
   if (!op.active()) return;  // uniform across the grid
   for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
-    const int sb = P.task_begin[task];
-    const int ns = P.task_begin[task + 1] - sb;
+    const int sb = cload(P.task_begin, task);
+    const int ns = cload(P.task_begin, task + 1) - sb;
+    if (ns == 1) {
+      // one (large) tensor segment: wave-uniform descriptor in SGPRs
+      const CONST_AS Seg* q = ((const CONST_AS Seg*)(P.segs)) + sb;
+      const int t = q->tensor;
+      const int64_t ub = q->unit_begin;
+      const int units = q->units;
+      const int parts = q->pad;
+      TV v;
+#pragma unroll
+      for (int s = 0; s < GS_PLAN_SLOTS; ++s) v.ptr[s] = cload(P.ptrs, static_cast<int64_t>(s) * P.n + t);
+      v.numel = cload(P.numel, t);
+      v.off = cload(P.off, t);
+      v.align = cload(P.align, t);
+      v.pad = 0;
+      if (parts > 0) run_interleaved<ILP>(op, v, static_cast<int>(ub), parts, units, acc);
+      else run_units<ILP>(op, &v, &ub, nullptr, 1, units, acc);
+      continue;
+    }
     if (threadIdx.x < ns) {
       const Seg sg = P.segs[sb + threadIdx.x];
       const int t = sg.tensor;
@@ -722,7 +772,7 @@ int hip_plan_upload_static(gs_plan* p) {
   const size_t tb = table_bytes(p) + 16;
   HIP_RET(hipMalloc(&p->d_table, tb));
   HIP_RET(hipMemset(p->d_table, 0, tb));
-  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * kMaxGrid));
+  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * kGridLimit));
   HIP_RET(hipHostMalloc(&p->pinned, tb * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) {
     hipEvent_t ev;

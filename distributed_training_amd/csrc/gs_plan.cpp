@@ -117,16 +117,38 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
       task_units_req > 0 ? std::max<int64_t>(kUnit, task_units_req) : plan_task_units(total_units);
   task_units += task_units & 1;  // even (see the segment padding below)
   p->task_units = task_units;
+  static const bool interleave = [] {
+    const char* e = std::getenv("GS_INTERLEAVE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
   for (int t = 0; t < n_tensors; ++t) {
-    const int64_t units = (numels[t] + kUnit - 1) / kUnit;
+    int64_t units = (numels[t] + kUnit - 1) / kUnit;
+    if (units == 0) continue;
+    // even unit counts: an 8-element lane-step (two units) never straddles
+    // segments; the padding unit lies past the tensor's end and is masked
+    units += units & 1;
+    if (interleave && units > task_units) {
+      // a tensor larger than a task is shared by M single-segment tasks in
+      // interleaved chunks (part i takes lane-step chunks i, i+M, i+2M, ...):
+      // the M workgroups sweep the tensor front to back together instead of M
+      // far-apart streams (DRAM / Infinity-Cache locality; a torch-copy-like
+      // access pattern) — Seg.pad = M, unit_begin = i, units = the tensor's
+      const int64_t parts = (units + task_units - 1) / task_units;
+      for (int64_t i = 0; i < parts; ++i) {
+        Seg s{};
+        s.unit_begin = i;
+        s.tensor = t;
+        s.units = static_cast<int32_t>(units);
+        s.pad = static_cast<int32_t>(parts);
+        p->segs.push_back(s);
+      }
+      continue;
+    }
     for (int64_t u = 0; u < units; u += task_units) {
       Seg s{};
       s.unit_begin = u;
       s.tensor = t;
       s.units = static_cast<int32_t>(std::min<int64_t>(task_units, units - u));
-      // even unit counts: an 8-element lane-step (two units) never straddles
-      // segments; the padding unit lies past the tensor's end and is masked
-      s.units += s.units & 1;
       p->segs.push_back(s);
     }
   }
@@ -135,18 +157,24 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
   int32_t tc = 0;
   for (size_t i = 0; i < p->segs.size(); ++i) {
     Seg& s = p->segs[i];
-    if (tc > 0 && (tu + s.units > task_units || tc == kMaxSegPerTask)) {
+    const bool alone = s.pad > 0;  // interleaved parts always own a task
+    if (tc > 0 && (alone || tu + s.units > task_units || tc == kMaxSegPerTask)) {
       p->task_begin.push_back(static_cast<int32_t>(i));
       tu = 0;
       tc = 0;
     }
     s.task_off = static_cast<int32_t>(tu);
-    tu += s.units;
+    tu += alone ? task_units : s.units;  // a part fills its task
     ++tc;
   }
   if (!p->segs.empty()) p->task_begin.push_back(static_cast<int32_t>(p->segs.size()));
   const int n_tasks = static_cast<int>(p->task_begin.size()) - 1;
-  p->grid = std::max(1, std::min(n_tasks, kMaxGrid));
+  static const int grid_cap = [] {
+    const char* e = std::getenv("GS_MAX_GRID");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? static_cast<int>(std::min<long>(v, kGridLimit)) : kMaxGrid;
+  }();
+  p->grid = std::max(1, std::min(n_tasks, grid_cap));
   p->h_ptrs.assign(static_cast<size_t>(GS_PLAN_SLOTS) * n_tensors, nullptr);
   p->h_align.assign(n_tensors, 0u);
   if (device_kind == GS_DEV_HIP) {
