@@ -2,7 +2,8 @@
 the reference's GPU path for the same work (torch ops on the same device).
 
 For ResNet-50 / ResNet-152 parameter sets (real per-tensor shapes) it times,
-with HIP events on the stream each kernel is launched on:
+with HIP events on the stream each kernel is launched on (libgsync rows: the
+plan launch timer, events recorded by the library around each kernel):
 
   libgsync                         reference GPU path (torch 2.10 on ROCm)
   pack fp32 (x 1/ws)   8 B/param    per-param  torch.mul(grad, 1/ws, out=bucket_view)  (Reducer mark_variable_ready_dense)
@@ -27,6 +28,19 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 HBM_PEAK = 8000.0
+
+
+def timeit_plan(plan, fn, iters=20, warmup=3):
+    """libgsync launches: the plan launch timer (HIP events recorded by the
+    library right around each kernel on its stream)."""
+    for _ in range(warmup):
+        fn()
+    plan.timer_enable(iters)
+    for _ in range(iters):
+        fn()
+    ts = sorted(plan.timer_read())
+    plan.timer_enable(0)
+    return ts[len(ts) // 2], sum(ts) / len(ts)
 
 
 def timeit(fn, iters=20, warmup=3):
@@ -79,21 +93,21 @@ def main():
 
     plan.set_ptrs(1, grads)
     plan.set_ptrs(2, grads)
-    rec("pack_f32", 8 * n, *timeit(lambda: plan.pack(1, torch.float32, flat, 0.125, 1), args.iters), "libgsync")
-    rec("pack_f32_to_bf16", 6 * n, *timeit(lambda: plan.pack(1, torch.float32, flat16, 0.125, 1), args.iters), "libgsync")
-    rec("unpack_f32", 8 * n, *timeit(lambda: plan.unpack(flat, 2, torch.float32), args.iters), "libgsync")
+    rec("pack_f32", 8 * n, *timeit_plan(plan, lambda: plan.pack(1, torch.float32, flat, 0.125, 1), args.iters), "libgsync")
+    rec("pack_f32_to_bf16", 6 * n, *timeit_plan(plan, lambda: plan.pack(1, torch.float32, flat16, 0.125, 1), args.iters), "libgsync")
+    rec("unpack_f32", 8 * n, *timeit_plan(plan, lambda: plan.unpack(flat, 2, torch.float32), args.iters), "libgsync")
     sq = torch.zeros(1, device=dev)
-    rec("unpack_f32+sqnorm", 8 * n, *timeit(lambda: plan.unpack(flat, 2, torch.float32, sqnorm=sq), args.iters), "libgsync")
-    rec("sqnorm_f32", 4 * n, *timeit(lambda: plan.sqnorm(1, torch.float32, sq), args.iters), "libgsync")
+    rec("unpack_f32+sqnorm", 8 * n, *timeit_plan(plan, lambda: plan.unpack(flat, 2, torch.float32, sqnorm=sq), args.iters), "libgsync")
+    rec("sqnorm_f32", 4 * n, *timeit_plan(plan, lambda: plan.sqnorm(1, torch.float32, sq), args.iters), "libgsync")
     plan.set_ptrs(0, params)
     plan.set_ptrs(1, grads)
     plan.set_ptrs(2, bufs)
-    rec("sgd_momentum_wd", 20 * n, *timeit(lambda: plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False),
-                                           args.iters), "libgsync")
+    rec("sgd_momentum_wd", 20 * n, *timeit_plan(plan, lambda: plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False),
+                                                args.iters), "libgsync")
     plan.set_ptrs(2, ms)
     plan.set_ptrs(3, vs)
-    rec("adam", 28 * n, *timeit(lambda: plan.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5),
-                                args.iters), "libgsync")
+    rec("adam", 28 * n, *timeit_plan(plan, lambda: plan.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5),
+                                     args.iters), "libgsync")
     if not args.skip_torch:
         inv = 1.0 / 8
 
