@@ -61,6 +61,7 @@ SIGNATURES = {
     "gs_version": (_c_int, []),
     "gs_last_error": (ctypes.c_char_p, []),
     "gs_device_count": (_c_int, []),
+    "gs_set_host_threads": (_c_int, [_c_int]),
     "gs_comm_unique_id_bytes": (_c_int, []),
     "gs_comm_get_unique_id": (_c_int, [_p_u8]),
     "gs_comm_create": (_c_int, [_c_int, _c_int, _p_u8, _c_int, _p_vp]),

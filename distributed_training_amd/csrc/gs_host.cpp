@@ -3,7 +3,17 @@
 // element for element (explicit fmaf, -ffp-contract=off), so a CPU run and a
 // GPU run of the engine agree bit for bit on the pack / unpack / optimizer
 // math.  A HIP plan never reaches this file.
+//
+// Speed: loops are instantiated per dtype combination (no per-element type
+// switch) so the compiler vectorises them (built with -mavx2 -mfma: std::fmaf
+// is one vfmadd, bit-identical to the software fmaf), and large plans are
+// split over gs_set_host_threads() threads (torch's intra-op thread count).
+// Elementwise results do not depend on the split; the Σg² reductions stay
+// serial (their double-precision order is the oracle's).
+#include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <thread>
 
 #include "gs_common.h"
 
@@ -34,24 +44,24 @@ inline uint16_t f32_to_f16(float f) {
   return h;
 }
 
-inline float ld(const void* base, int dt, int64_t i) {
-  switch (dt) {
-    case GS_F32: return static_cast<const float*>(base)[i];
-    case GS_BF16: return bf16_to_f32(static_cast<const uint16_t*>(base)[i]);
-    default: return f16_to_f32(static_cast<const uint16_t*>(base)[i]);
-  }
+
+template <int DT>
+inline float ldT(const void* base, int64_t i) {
+  if constexpr (DT == GS_F32) return static_cast<const float*>(base)[i];
+  else if constexpr (DT == GS_BF16) return bf16_to_f32(static_cast<const uint16_t*>(base)[i]);
+  else return f16_to_f32(static_cast<const uint16_t*>(base)[i]);
 }
-inline void st(void* base, int dt, int64_t i, float v) {
-  switch (dt) {
-    case GS_F32: static_cast<float*>(base)[i] = v; break;
-    case GS_BF16: static_cast<uint16_t*>(base)[i] = f32_to_bf16(v); break;
-    default: static_cast<uint16_t*>(base)[i] = f32_to_f16(v); break;
-  }
+template <int DT>
+inline void stT(void* base, int64_t i, float v) {
+  if constexpr (DT == GS_F32) static_cast<float*>(base)[i] = v;
+  else if constexpr (DT == GS_BF16) static_cast<uint16_t*>(base)[i] = f32_to_bf16(v);
+  else static_cast<uint16_t*>(base)[i] = f32_to_f16(v);
 }
-inline float round_to(int dt, float v) {
-  if (dt == GS_F32) return v;
-  if (dt == GS_BF16) return bf16_to_f32(f32_to_bf16(v));
-  return f16_to_f32(f32_to_f16(v));
+template <int DT>
+inline float roundT(float v) {
+  if constexpr (DT == GS_F32) return v;
+  else if constexpr (DT == GS_BF16) return bf16_to_f32(f32_to_bf16(v));
+  else return f16_to_f32(f32_to_f16(v));
 }
 inline void* slot(gs_plan* p, int s, int t) { return p->h_ptrs[static_cast<size_t>(s) * p->n + t]; }
 
@@ -60,90 +70,149 @@ int check_float(int dt) {
   return GS_OK;
 }
 
+std::atomic<int> g_threads{1};
+constexpr int64_t kChunk = int64_t(1) << 16;     // elements per work item
+constexpr int64_t kParallelMin = int64_t(1) << 19;  // below this, one thread
+
+// fn(t, i0, i1) over every tensor's element range, split into chunks and
+// spread over the host threads (static round-robin: deterministic, and the
+// elementwise results do not depend on it anyway)
+template <class F>
+void for_ranges(const gs_plan* p, F&& fn) {
+  int64_t total = 0;
+  for (int t = 0; t < p->n; ++t) total += p->numel[t];
+  const int nt = std::max(1, std::min<int>(g_threads.load(), static_cast<int>(total / kChunk) + 1));
+  if (nt == 1 || total < kParallelMin) {
+    for (int t = 0; t < p->n; ++t)
+      if (p->numel[t]) fn(t, int64_t(0), p->numel[t]);
+    return;
+  }
+  std::vector<std::tuple<int, int64_t, int64_t>> items;
+  for (int t = 0; t < p->n; ++t)
+    for (int64_t i = 0; i < p->numel[t]; i += kChunk) items.emplace_back(t, i, std::min(p->numel[t], i + kChunk));
+  auto work = [&](int k) {
+    for (size_t j = k; j < items.size(); j += nt) fn(std::get<0>(items[j]), std::get<1>(items[j]), std::get<2>(items[j]));
+  };
+  std::vector<std::thread> pool;
+  for (int k = 1; k < nt; ++k) pool.emplace_back(work, k);
+  work(0);
+  for (auto& th : pool) th.join();
+}
+
+#define GS_HOST_FLOAT(DT, NAME, ...)                                    \
+  switch (DT) {                                                         \
+    case GS_F32: { constexpr int NAME = GS_F32; __VA_ARGS__; break; }   \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; } \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }   \
+    default: return fail(GS_EINVAL, "unsupported floating dtype");      \
+  }
+#define GS_HOST_LOWP(DT, NAME, ...)                                      \
+  switch (DT) {                                                          \
+    case -1: { constexpr int NAME = -1; __VA_ARGS__; break; }            \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; }  \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }    \
+    default: return fail(GS_EINVAL, "unsupported low-precision dtype");  \
+  }
+
 }  // namespace
 
 int host_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode) {
-  GS_TRY_RET(check_float(src_dt));
-  GS_TRY_RET(check_float(flat_dt));
-  const int fsz = dtype_size(flat_dt);
-  for (int t = 0; t < p->n; ++t) {
-    const void* src = slot(p, src_slot, t);
-    void* dst = static_cast<char*>(flat) + p->off[t] * fsz;
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      float v = src ? ld(src, src_dt, i) : 0.f;
-      if (mode == GS_SCALE_MUL) v = v * s;
-      else if (mode == GS_SCALE_DIV) v = round_to(flat_dt, v) / s;
-      st(dst, flat_dt, i, v);
-    }
-  }
+  GS_HOST_FLOAT(src_dt, SD, GS_HOST_FLOAT(flat_dt, FD, {
+    const int fsz = dtype_size(FD);
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      const void* src = slot(p, src_slot, t);
+      void* dst = static_cast<char*>(flat) + p->off[t] * fsz;
+      if (!src) {
+        const float z = mode == GS_SCALE_MUL ? 0.f * s : (mode == GS_SCALE_DIV ? 0.f / s : 0.f);
+        for (int64_t i = i0; i < i1; ++i) stT<FD>(dst, i, z);  // unused parameter: zeros, as the kernel
+      } else if (mode == GS_SCALE_MUL) {
+        for (int64_t i = i0; i < i1; ++i) stT<FD>(dst, i, ldT<SD>(src, i) * s);
+      } else if (mode == GS_SCALE_DIV) {
+        for (int64_t i = i0; i < i1; ++i) stT<FD>(dst, i, roundT<FD>(ldT<SD>(src, i)) / s);
+      } else {
+        for (int64_t i = i0; i < i1; ++i) stT<FD>(dst, i, ldT<SD>(src, i));
+      }
+    });
+  }));
   return GS_OK;
 }
 
 int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
                 int acc) {
-  GS_TRY_RET(check_float(flat_dt));
-  GS_TRY_RET(check_float(dst_dt));
-  const int fsz = dtype_size(flat_dt);
-  double total = 0.0;
-  for (int t = 0; t < p->n; ++t) {
-    const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
-    void* dst = slot(p, dst_slot, t);
-    if (dst == nullptr) continue;
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      const float v = ld(src, flat_dt, i);
-      st(dst, dst_dt, i, v);
-      if (sq) {
-        const float r = round_to(dst_dt, v);
-        total += static_cast<double>(r) * r;
+  GS_HOST_FLOAT(flat_dt, FD, GS_HOST_FLOAT(dst_dt, DD, {
+    const int fsz = dtype_size(FD);
+    if (sq) {  // serial: the double-precision Σ order is the oracle's
+      double total = 0.0;
+      for (int t = 0; t < p->n; ++t) {
+        const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
+        void* dst = slot(p, dst_slot, t);
+        if (dst == nullptr) continue;
+        for (int64_t i = 0; i < p->numel[t]; ++i) {
+          const float v = ldT<FD>(src, i);
+          stT<DD>(dst, i, v);
+          const float r = roundT<DD>(v);
+          total += static_cast<double>(r) * r;
+        }
       }
+      sq[0] = acc ? sq[0] + static_cast<float>(total) : static_cast<float>(total);
+    } else {
+      for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+        const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
+        void* dst = slot(p, dst_slot, t);
+        if (dst == nullptr) return;
+        for (int64_t i = i0; i < i1; ++i) stT<DD>(dst, i, ldT<FD>(src, i));
+      });
     }
-  }
-  if (sq) sq[0] = acc ? sq[0] + static_cast<float>(total) : static_cast<float>(total);
+  }));
   return GS_OK;
 }
 
 int host_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found) {
-  GS_TRY_RET(check_float(flat_dt));
-  GS_TRY_RET(check_float(dst_dt));
-  const int fsz = dtype_size(flat_dt);
-  float f = found[0];
-  for (int t = 0; t < p->n; ++t) {
-    const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
-    void* dst = slot(p, dst_slot, t);
-    if (dst == nullptr) continue;
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      const float v = ld(src, flat_dt, i);
-      st(dst, dst_dt, i, v);
-      if (!std::isfinite(round_to(dst_dt, v))) f = 1.f;
-    }
-  }
-  found[0] = f;
+  std::atomic<int> bad{found[0] != 0.f ? 1 : 0};
+  GS_HOST_FLOAT(flat_dt, FD, GS_HOST_FLOAT(dst_dt, DD, {
+    const int fsz = dtype_size(FD);
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      const void* src = static_cast<const char*>(flat) + p->off[t] * fsz;
+      void* dst = slot(p, dst_slot, t);
+      if (dst == nullptr) return;
+      int b = 0;
+      for (int64_t i = i0; i < i1; ++i) {
+        const float v = ldT<FD>(src, i);
+        stT<DD>(dst, i, v);
+        b |= !std::isfinite(roundT<DD>(v));
+      }
+      if (b) bad.store(1);
+    });
+  }));
+  found[0] = bad.load() ? 1.f : 0.f;
   return GS_OK;
 }
 
 int host_scale(gs_plan* p, int s_, int dt, float s, int mode) {
-  GS_TRY_RET(check_float(dt));
-  for (int t = 0; t < p->n; ++t) {
-    void* x = slot(p, s_, t);
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      const float v = ld(x, dt, i);
-      st(x, dt, i, mode == GS_SCALE_DIV ? v / s : v * s);
-    }
-  }
+  GS_HOST_FLOAT(dt, DT, {
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      void* x = slot(p, s_, t);
+      if (mode == GS_SCALE_DIV)
+        for (int64_t i = i0; i < i1; ++i) stT<DT>(x, i, ldT<DT>(x, i) / s);
+      else
+        for (int64_t i = i0; i < i1; ++i) stT<DT>(x, i, ldT<DT>(x, i) * s);
+    });
+  });
   return GS_OK;
 }
 
 int host_sqnorm(gs_plan* p, int s_, int dt, float* sq, int acc) {
-  GS_TRY_RET(check_float(dt));
-  double total = 0.0;
-  for (int t = 0; t < p->n; ++t) {
-    const void* x = slot(p, s_, t);
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      const double v = ld(x, dt, i);
-      total += v * v;
+  GS_HOST_FLOAT(dt, DT, {
+    double total = 0.0;
+    for (int t = 0; t < p->n; ++t) {
+      const void* x = slot(p, s_, t);
+      for (int64_t i = 0; i < p->numel[t]; ++i) {
+        const double v = ldT<DT>(x, i);
+        total += v * v;
+      }
     }
-  }
-  sq[0] = acc ? sq[0] + static_cast<float>(total) : static_cast<float>(total);
+    sq[0] = acc ? sq[0] + static_cast<float>(total) : static_cast<float>(total);
+  });
   return GS_OK;
 }
 
@@ -156,76 +225,98 @@ int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, floa
 }
 
 int host_unscale_check(gs_plan* p, int s_, int dt, const float* inv, float* found) {
-  GS_TRY_RET(check_float(dt));
-  float f = found[0];
-  for (int t = 0; t < p->n; ++t) {
-    void* x = slot(p, s_, t);
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      const float v = ld(x, dt, i);
-      if (!std::isfinite(v)) f = 1.f;
-      if (inv && inv[0] != 1.f) st(x, dt, i, v * inv[0]);
-    }
-  }
-  found[0] = f;
+  std::atomic<int> bad{found[0] != 0.f ? 1 : 0};
+  const bool scale = inv && inv[0] != 1.f;
+  const float sc = scale ? inv[0] : 1.f;
+  GS_HOST_FLOAT(dt, DT, {
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      void* x = slot(p, s_, t);
+      int b = 0;
+      for (int64_t i = i0; i < i1; ++i) {
+        const float v = ldT<DT>(x, i);
+        b |= !std::isfinite(v);
+        if (scale) stT<DT>(x, i, v * sc);
+      }
+      if (b) bad.store(1);
+    });
+  });
+  found[0] = bad.load() ? 1.f : 0.f;
   return GS_OK;
 }
 
 int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi) {
-  GS_TRY_RET(check_float(gdt));
-  if (fi && fi[0] != 0.f) return GS_OK;
-  for (int t = 0; t < p->n; ++t) {
-    float* pp = static_cast<float*>(slot(p, 0, t));
-    const void* gp = slot(p, 1, t);
-    float* bp = static_cast<float*>(slot(p, 2, t));
-    void* lp = slot(p, 3, t);
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      float g = ld(gp, gdt, i);
-      if (gsc) g = g * gsc[0];
-      if (h.maximize) g = -g;
-      if (h.wd != 0.f) g = std::fmaf(h.wd, pp[i], g);
-      float d = g;
-      if (h.mom != 0.f) {
-        const float b = h.first ? g : std::fmaf(h.omd, g, bp[i] * h.mom);
-        bp[i] = b;
-        d = h.nesterov ? std::fmaf(h.mom, b, g) : b;
-      }
-      pp[i] = std::fmaf(-h.lr, d, pp[i]);
-      if (ldt >= 0) st(lp, ldt, i, pp[i]);
-    }
+  if (fi && fi[0] != 0.f) {
+    GS_TRY_RET(check_float(gdt));
+    return GS_OK;
   }
+  const bool has_gs = gsc != nullptr;
+  const float gs = has_gs ? gsc[0] : 1.f;
+  GS_HOST_FLOAT(gdt, GD, GS_HOST_LOWP(ldt, LD, {
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      float* pp = static_cast<float*>(slot(p, 0, t));
+      const void* gp = slot(p, 1, t);
+      float* bp = static_cast<float*>(slot(p, 2, t));
+      void* lp = slot(p, 3, t);
+      for (int64_t i = i0; i < i1; ++i) {
+        float g = ldT<GD>(gp, i);
+        if (has_gs) g = g * gs;
+        if (h.maximize) g = -g;
+        if (h.wd != 0.f) g = std::fmaf(h.wd, pp[i], g);
+        float d = g;
+        if (h.mom != 0.f) {
+          const float b = h.first ? g : std::fmaf(h.omd, g, bp[i] * h.mom);
+          bp[i] = b;
+          d = h.nesterov ? std::fmaf(h.mom, b, g) : b;
+        }
+        pp[i] = std::fmaf(-h.lr, d, pp[i]);
+        if constexpr (LD >= 0) stT<LD>(lp, i, pp[i]);
+      }
+    });
+  }));
   return GS_OK;
 }
 
 int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc,
               const float* fi) {
-  GS_TRY_RET(check_float(gdt));
-  if (fi && fi[0] != 0.f) return GS_OK;
-  for (int t = 0; t < p->n; ++t) {
-    float* pp = static_cast<float*>(slot(p, 0, t));
-    const void* gp = slot(p, 1, t);
-    float* mp = static_cast<float*>(slot(p, 2, t));
-    float* vp = static_cast<float*>(slot(p, 3, t));
-    void* lp = slot(p, 4, t);
-    for (int64_t i = 0; i < p->numel[t]; ++i) {
-      float g = ld(gp, gdt, i);
-      if (gsc) g = g * gsc[0];
-      if (h.maximize) g = -g;
-      float x = pp[i];
-      if (h.wd != 0.f) {
-        if (h.adamw) x = x * h.decay;
-        else g = std::fmaf(h.wd, x, g);
-      }
-      const float m = std::fmaf(h.w1, g - mp[i], mp[i]);
-      const float v = std::fmaf(h.w2 * g, g, vp[i] * h.b2);
-      const float denom = std::sqrt(v) / h.bc2s + h.eps;
-      x = std::fmaf(h.step_size, m / denom, x);
-      pp[i] = x;
-      mp[i] = m;
-      vp[i] = v;
-      if (ldt >= 0) st(lp, ldt, i, x);
-    }
+  if (fi && fi[0] != 0.f) {
+    GS_TRY_RET(check_float(gdt));
+    return GS_OK;
   }
+  const bool has_gs = gsc != nullptr;
+  const float gs = has_gs ? gsc[0] : 1.f;
+  GS_HOST_FLOAT(gdt, GD, GS_HOST_LOWP(ldt, LD, {
+    for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
+      float* pp = static_cast<float*>(slot(p, 0, t));
+      const void* gp = slot(p, 1, t);
+      float* mp = static_cast<float*>(slot(p, 2, t));
+      float* vp = static_cast<float*>(slot(p, 3, t));
+      void* lp = slot(p, 4, t);
+      for (int64_t i = i0; i < i1; ++i) {
+        float g = ldT<GD>(gp, i);
+        if (has_gs) g = g * gs;
+        if (h.maximize) g = -g;
+        float x = pp[i];
+        if (h.wd != 0.f) {
+          if (h.adamw) x = x * h.decay;
+          else g = std::fmaf(h.wd, x, g);
+        }
+        const float m = std::fmaf(h.w1, g - mp[i], mp[i]);
+        const float v = std::fmaf(h.w2 * g, g, vp[i] * h.b2);
+        const float denom = std::sqrt(v) / h.bc2s + h.eps;
+        x = std::fmaf(h.step_size, m / denom, x);
+        pp[i] = x;
+        mp[i] = m;
+        vp[i] = v;
+        if constexpr (LD >= 0) stT<LD>(lp, i, x);
+      }
+    });
+  }));
   return GS_OK;
 }
 
 }  // namespace gs
+
+extern "C" int gs_set_host_threads(int n) {
+  gs::g_threads.store(n < 1 ? 1 : (n > 256 ? 256 : n));
+  return GS_OK;
+}

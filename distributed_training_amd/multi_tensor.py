@@ -57,6 +57,8 @@ class TensorListPlan:
     def _stream(self, stream):
         if stream is not None:
             return stream
+        if self.kind == L.GS_DEV_HOST:  # host backend: torch's intra-op threads
+            L.lib().gs_set_host_threads(torch.get_num_threads())
         return L.stream_ptr(self.device)
 
     def set_ptrs(self, slot: int, tensors_or_ptrs):

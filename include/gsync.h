@@ -52,6 +52,10 @@ extern "C" {
 #define GS_I32 5
 #define GS_U8 6
 
+/* threads the host implementation (GS_DEV_HOST plans) may use; torch's
+ * intra-op thread count is passed by the Python layer (default 1) */
+int gs_set_host_threads(int n);
+
 /* ---- device kinds ---- */
 #define GS_DEV_HOST 0
 #define GS_DEV_HIP 1

@@ -303,3 +303,38 @@ def test_plan_task_sizing():
     assert huge.task_units == 4096
     with pytest.raises(L.GsyncError, match="host plans"):
         small.timer_enable(4)
+
+
+def test_host_threads_bitwise():
+    """The host backend's threaded loops (gs_set_host_threads) give the same bits
+    as one thread: every op is elementwise, the split only changes who computes."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.multi_tensor import TensorListPlan
+
+    sizes = [1_000_003, 7, 300_000, 65_536 * 3 + 5]
+    g = torch.Generator().manual_seed(0)
+
+    def run(threads):
+        torch.manual_seed(0)
+        ps = [torch.randn(n, generator=torch.Generator().manual_seed(i)) for i, n in enumerate(sizes)]
+        gs = [torch.randn(n, generator=torch.Generator().manual_seed(10 + i)) * 0.01 for i, n in enumerate(sizes)]
+        ms = [torch.zeros(n) for n in sizes]
+        vs = [torch.zeros(n) for n in sizes]
+        plan = TensorListPlan(sizes, torch.device("cpu"), align=64)
+        for k, ts in enumerate((ps, gs, ms, vs)):
+            plan.set_ptrs(k, ts)
+        flat = torch.zeros(plan.flat_numel, dtype=torch.bfloat16)
+        old = torch.get_num_threads()
+        torch.set_num_threads(threads)  # the Python layer forwards it to the library
+        try:
+            plan.pack(1, torch.float32, flat, 0.25, L.GS_SCALE_MUL)
+            plan.adam(torch.float32, 1e-3, 0.9, 0.999, 1e-8, 1e-2, True, False, -1e-3, 0.7)
+            found = torch.zeros(1)
+            plan.unscale_check(1, torch.float32, torch.tensor([0.5]), found)
+        finally:
+            torch.set_num_threads(old)
+        return [flat.clone()] + ps + ms + vs + gs + [found]
+
+    a, b = run(1), run(8)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
