@@ -76,6 +76,19 @@ def compute_bucket_assignment_by_size(tensors, size_limits, order=None):
     return out
 
 
+def _as_words(t: torch.Tensor):
+    """A view of buffer `t` the multi-tensor kernels can move bit for bit:
+    fp32 / bf16 / fp16 as they are; 4- and 8-byte integer or fp64 tensors as
+    fp32 words (pure loads and stores, no arithmetic); None otherwise."""
+    if not t.is_contiguous():
+        return None
+    if t.dtype in (torch.float32, torch.bfloat16, torch.float16):
+        return t
+    if t.element_size() in (4, 8) and t.dtype != torch.complex64:
+        return t.reshape(-1).view(torch.float32)
+    return None
+
+
 class GradBucket:
     """Mirror of torch.distributed.GradBucket (T:include/torch/csrc/distributed/c10d/comm.hpp:20-98)."""
 
@@ -346,26 +359,33 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _sync_buffers(self):
-        """Per-forward BN buffer broadcast (T:nn/parallel/distributed.py:2178-2221),
-        pack kernel + one collective + unpack, plan cached across steps."""
+        """Per-forward BN buffer broadcast (T:nn/parallel/distributed.py:2178-2221):
+        one pack launch + one RCCL broadcast + one unpack launch per word size,
+        plan cached across steps.  Integer buffers (BN num_batches_tracked,
+        int64) travel as fp32 words — the kernels move them bit for bit."""
         bufs = self._module_buffers()
         if self.world_size == 1 or not bufs:
             return
-        floats = [t for t in bufs if t.is_floating_point() and is_dense(t)]
-        others = [t for t in bufs if not (t.is_floating_point() and is_dense(t))]
         key = tuple(id(t) for t in bufs)
         if self._buffers_plan is None or self._buffers_plan[0] != key:
+            groups: dict = {}
+            others = []
+            for t in bufs:
+                w = _as_words(t)
+                if w is None:
+                    others.append(t)
+                else:
+                    groups.setdefault(w.dtype, []).append(w)
             plans = []
-            by_dtype: dict = {}
-            for t in floats:
-                by_dtype.setdefault(t.dtype, []).append(t)
-            for dt, ts in by_dtype.items():
-                plan = TensorListPlan([t.numel() for t in ts], self.device, align=BUCKET_ALIGN_ELEMS)
+            for dt, ws in groups.items():
+                plan = TensorListPlan([w.numel() for w in ws], self.device, align=BUCKET_ALIGN_ELEMS)
                 flat = torch.zeros(plan.flat_numel, dtype=dt, device=self.device)
-                plans.append((plan, ts, dt, flat))
-            self._buffers_plan = (key, plans)
-        for plan, ts, dt, flat in self._buffers_plan[1]:
-            plan.set_ptrs(0, ts)
+                plan.set_ptrs(0, ws)
+                plans.append((plan, ws, dt, flat))
+            self._buffers_plan = (key, plans, others)
+        _, plans, others = self._buffers_plan
+        for plan, ws, dt, flat in plans:
+            plan.set_ptrs(0, ws)
             if self.rank == 0:
                 plan.pack(0, dt, flat)
             self._bcast_flat(flat)
