@@ -84,6 +84,9 @@ SIGNATURES = {
     "gs_plan_offsets": (_c_int, [_vp, _p_i64]),
     "gs_plan_n_tasks": (_c_int, [_vp]),
     "gs_plan_task_units": (_c_i64, [_vp]),
+    "gs_plan_set_hyper_source": (_c_int, [_vp, _vp]),
+    "gs_watchdog_pause": (_c_int, [_c_int]),
+    "gs_adam_hyper": (_c_int, [_c_int, _vp, _vp, _c_d, _c_d, _c_d, _vp, _vp, _vp]),
     "gs_plan_timer_enable": (_c_int, [_vp, _c_int]),
     "gs_plan_timer_read": (_c_int, [_vp, _p_f, _p_i32, _c_int]),
     "gs_plan_set_ptrs": (_c_int, [_vp, _c_int, _p_vp, _vp]),

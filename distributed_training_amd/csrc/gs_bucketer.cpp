@@ -169,10 +169,12 @@ int launch_bucket(gs_bucketer* b, int bi) {
     HIPB_RET(hipEventRecord(bk.ev_ready, static_cast<hipStream_t>(b->producer)));
     HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
     GS_TRY_RET(pack_one(b, bk, cs));
-    HIPB_RET(hipEventRecord(bk.ev_t0, cs));
+    // timing events stay out of a hipGraph capture (last_comm_ms then reports -1)
+    const bool timed = !stream_capturing(cs);
+    if (timed) HIPB_RET(hipEventRecord(bk.ev_t0, cs));
     GS_TRY_RET(launch_collective(b, bk, cs));
-    HIPB_RET(hipEventRecord(bk.ev_t1, cs));
-    bk.timed = true;
+    if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
+    bk.timed = timed;
     if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
   } else {
     GS_TRY_RET(pack_one(b, bk, b->producer));

@@ -101,11 +101,16 @@ void abort_locked(gs_comm* c, const std::string& why) {
   if (c->comm) (void)ncclCommAbort(c->comm);
 }
 
+// > 0 while a graph capture is being recorded (gs_watchdog_pause): event
+// queries from the watchdog thread are not allowed during a global-mode capture
+std::atomic<int> g_wd_pause{0};
+
 void watchdog_loop(gs_comm* c) {
   (void)hipSetDevice(c->device);
   using clk = std::chrono::steady_clock;
   while (!c->wd_stop.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    if (g_wd_pause.load() > 0) continue;
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->aborted.load()) continue;
     ncclResult_t async = ncclSuccess;
@@ -143,7 +148,8 @@ int comm_check_live(gs_comm* c) {
 
 // after enqueueing a collective on `stream`: hand its completion to the watchdog
 int comm_track(gs_comm* c, hipStream_t stream) {
-  if (c->timeout_ms <= 0) return GS_OK;
+  // a collective recorded into a hipGraph runs at replay, not now: not tracked
+  if (c->timeout_ms <= 0 || stream_capturing(stream)) return GS_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   hipEvent_t ev;
   if (!c->ev_pool.empty()) {
@@ -224,6 +230,15 @@ int gs_comm_abort(gs_comm* c) {
   GS_CHECK_ARG(c != nullptr, "gs_comm_abort: NULL comm");
   std::lock_guard<std::mutex> lk(c->mu);
   abort_locked(c, "aborted by the caller (gs_comm_abort)");
+  return GS_OK;
+}
+
+int gs_watchdog_pause(int pause) {
+  const int v = pause ? g_wd_pause.fetch_add(1) + 1 : g_wd_pause.fetch_sub(1) - 1;
+  if (v < 0) {
+    g_wd_pause.store(0);
+    return fail(GS_ESTATE, "gs_watchdog_pause: resume without a pause");
+  }
   return GS_OK;
 }
 

@@ -1,6 +1,7 @@
 // Internal declarations shared by the libgsync translation units.
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -130,6 +131,10 @@ struct gs_plan {
   void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};
   void* last_stream = nullptr;
   void* last_event = nullptr;
+  bool last_captured = false;   // the last launch was recorded into a stream capture
+  unsigned long long table_capture_id = 0;  // capture that last recorded a table write
+  bool in_graph = false;        // a graph holds a table write: re-upload before eager launches
+  const float* hyper = nullptr; // device hyper-parameter source of sgd/adam (gs_plan_set_hyper_source)
   // launch timer ring (gs_plan_timer_enable)
   std::vector<void*> timer_ev;  // [2 * slots]: start, stop
   std::vector<int32_t> timer_kind;  // [slots]: GS_OP_* of the timed launch
@@ -168,10 +173,27 @@ GS_HD inline float aug_pixel(const uint8_t* src, int64_t idx, int H, int W, int 
 }
 int hip_image_augment(int device, const ImageAugArgs& a, void* stream);
 
+// Adam's step-varying hyper-parameters from a device step counter (torch's
+// capturable=True): step += 1 unless found_inf; then, in double as the host
+// path forms them, hyper = [-(lr/bc1), sqrt(bc2), 1 - lr*wd] rounded to fp32.
+GS_HD inline void adam_hyper_update(double* step, const double* lr, double beta1, double beta2,
+                                    double wd, const float* found_inf, float* hyper) {
+  double s = step[0];
+  if (found_inf == nullptr || found_inf[0] == 0.f) s += 1.0;
+  step[0] = s;
+  const double bc1 = 1.0 - pow(beta1, s), bc2 = 1.0 - pow(beta2, s);
+  hyper[0] = static_cast<float>((lr[0] / bc1) * -1.0);
+  hyper[1] = static_cast<float>(sqrt(bc2));
+  hyper[2] = static_cast<float>(1.0 - lr[0] * wd);
+}
+int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, double wd,
+                   const float* found_inf, float* hyper, void* stream);
+
 // HIP-side implementations (gs_kernels.hip)
 int hip_plan_upload_static(gs_plan* p);
 int hip_plan_release(gs_plan* p);
 int hip_plan_flush(gs_plan* p, void* stream);
+bool stream_capturing(void* stream);  // hipStreamIsCapturing: recording into a hipGraph
 int hip_plan_timer_enable(gs_plan* p, int n_slots);
 int hip_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap);
 int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,

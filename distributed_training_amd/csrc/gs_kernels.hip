@@ -280,11 +280,16 @@ struct TV {
 
 // Op contract:
 //   struct Frag;                             registers for one unit (4 elements)
+//   load_hyper(Op&) overload (optional)      step-varying hyper-parameters from device memory
 //   bool active() const;                     uniform early-out (found_inf skip)
 //   void load(const TV&, e, Frag&)           issue the unit's loads
 //   void apply(const TV&, e, Frag&, acc)     compute + store (+ reduction)
 //   static constexpr int kRed = 0 (none) | 1 (sum) | 2 (max); float* partials
 //   static constexpr int kKind = GS_OP_* (tags the launch timer's records)
+// default: hyper-parameters travel in the kernel arguments
+template <class Op>
+__device__ __forceinline__ void load_hyper(Op&) {}
+
 template <int ILP, class Op>
 __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
                                           const int32_t* s_pref, int ns, int total, float& acc) {
@@ -375,6 +380,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
   __shared__ int32_t s_pref[kMaxSegPerTask + 1];
   float acc = 0.f;
   if (!op.active()) return;  // uniform across the grid
+  load_hyper(op);             // uniform: graph-replayable lr / bias corrections
   for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
     const int sb = cload(P.task_begin, task);
     const int ns = cload(P.task_begin, task + 1) - sb;
@@ -588,6 +594,7 @@ struct SgdOp {
   SgdHyper h;
   const float* gscale;
   const float* found_inf;
+  const float* hyper = nullptr;  // [lr] in device memory (gs_plan_set_hyper_source)
   struct Frag { float p[N], g[N], b[N]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
@@ -628,6 +635,7 @@ struct AdamOp {
   AdamHyper h;
   const float* gscale;
   const float* found_inf;
+  const float* hyper = nullptr;  // [step_size, bc2_sqrt, 1 - lr*wd] in device memory
   struct Frag { float p[N], g[N], m[N], v[N]; };
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
   __device__ void load(const TV& tv, int64_t e, Frag& f) const {
@@ -660,6 +668,19 @@ struct AdamOp {
     if constexpr (LD >= 0) storeN<LD, N>(tv.ptr[4], e, tv.numel, tv.vec(4), f.p);
   }
 };
+
+template <int N, int GD, int LD>
+__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD>& op) {
+  if (op.hyper) op.h.lr = op.hyper[0];
+}
+template <int N, int GD, int LD>
+__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD>& op) {
+  if (op.hyper) {
+    op.h.step_size = op.hyper[0];
+    op.h.bc2s = op.hyper[1];
+    op.h.decay = op.hyper[2];
+  }
+}
 
 __global__ void clip_coef_kernel(const float* sq, float max_norm, float eps, float* coef,
                                  float* norm) {
@@ -695,7 +716,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   GS_TRY_RET(hip_plan_flush(p, stream));
   op.partials = p->d_partials;
-  const int nslots = static_cast<int>(p->timer_ev.size() / 2);
+  const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
   if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
   hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(p->grid), dim3(kBlock), 0, s, p->args(), op);
@@ -715,6 +736,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), s));
   p->last_stream = stream;
+  p->last_captured = stream_capturing(s);
   return GS_OK;
 }
 
@@ -842,19 +864,73 @@ int hip_plan_release(gs_plan* p) {
   return GS_OK;
 }
 
+// Table upload while the stream is being captured into a hipGraph: the table
+// travels in kernel arguments (captured by value), ~3 KiB per launch, so the
+// graph carries no reference to host staging memory and no host sync is
+// needed; a replay rewrites the same (static) pointers.
+constexpr int kTableWordsPerLaunch = 384;  // 3 KiB of 8-byte words
+struct TableChunk {
+  uint64_t words[kTableWordsPerLaunch];
+  int64_t first;  // first 8-byte word of the table this chunk writes
+  int32_t count;
+};
+__global__ void __launch_bounds__(128) table_write_kernel(uint64_t* table, TableChunk c) {
+  for (int i = threadIdx.x; i < c.count; i += blockDim.x) table[c.first + i] = c.words[i];
+}
+
+bool stream_capturing(void* stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(static_cast<hipStream_t>(stream), &st) == hipSuccess &&
+         st == hipStreamCaptureStatusActive;
+}
+
+// Pointer-table upload before a launch.  Eager: staged through a pinned ring
+// and copied on the launch stream.  Under hipGraph capture: written by
+// table_write_kernel launches (once per plan per capture), so every replay
+// restores the table the captured kernels were recorded against even if eager
+// launches changed it in between; the plan then re-uploads before its next
+// eager launch, since a replay may have overwritten the eager table.
 int hip_plan_flush(gs_plan* p, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // a launch on a new stream is ordered after the plan's previous launch
-  if (p->last_stream != nullptr && p->last_stream != stream)
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(s, &st, &cid) != hipSuccess) st = hipStreamCaptureStatusNone;
+  const bool capturing = st == hipStreamCaptureStatusActive;
+  // a launch on a new stream is ordered after the plan's previous launch when
+  // both are eager or both belong to the capture (an event recorded inside a
+  // capture cannot order eager work: graph replays are ordered by the caller,
+  // as torch.cuda.graph requires)
+  if (p->last_stream != nullptr && p->last_stream != stream && capturing == p->last_captured &&
+      (!capturing || cid == p->table_capture_id))
     HIP_RET(hipStreamWaitEvent(s, static_cast<hipEvent_t>(p->last_event), 0));
-  if (!p->dirty) return GS_OK;
+  const size_t ptr_bytes = sizeof(void*) * GS_PLAN_SLOTS * p->n;
   const size_t tb = table_bytes(p);
+  if (capturing) {
+    if (!p->dirty && p->table_capture_id == cid) return GS_OK;
+    std::vector<uint64_t> words((tb + 7) / 8, 0);
+    std::memcpy(words.data(), p->h_ptrs.data(), ptr_bytes);
+    std::memcpy(reinterpret_cast<char*>(words.data()) + ptr_bytes, p->h_align.data(),
+                sizeof(uint32_t) * p->n);
+    for (size_t w = 0; w < words.size(); w += kTableWordsPerLaunch) {
+      TableChunk c{};
+      c.first = static_cast<int64_t>(w);
+      c.count = static_cast<int32_t>(std::min<size_t>(kTableWordsPerLaunch, words.size() - w));
+      std::memcpy(c.words, words.data() + w, sizeof(uint64_t) * c.count);
+      hipLaunchKernelGGL(table_write_kernel, dim3(1), dim3(128), 0, s,
+                         static_cast<uint64_t*>(p->d_table), c);
+      HIP_RET(hipGetLastError());
+    }
+    p->table_capture_id = cid;
+    p->in_graph = true;
+    p->dirty = false;
+    return GS_OK;
+  }
+  if (!p->dirty && !p->in_graph) return GS_OK;
   const int k = p->ring;
   HIP_RET(hipEventSynchronize(static_cast<hipEvent_t>(p->ring_events[k])));
   char* stage = static_cast<char*>(p->pinned) + k * (tb + 16);
-  std::memcpy(stage, p->h_ptrs.data(), sizeof(void*) * GS_PLAN_SLOTS * p->n);
-  std::memcpy(stage + sizeof(void*) * GS_PLAN_SLOTS * p->n, p->h_align.data(),
-              sizeof(uint32_t) * p->n);
+  std::memcpy(stage, p->h_ptrs.data(), ptr_bytes);
+  std::memcpy(stage + ptr_bytes, p->h_align.data(), sizeof(uint32_t) * p->n);
   HIP_RET(hipMemcpyAsync(p->d_table, stage, tb, hipMemcpyHostToDevice, s));
   HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->ring_events[k]), s));
   p->ring = (k + 1) & 3;
@@ -941,6 +1017,19 @@ int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float
   return GS_OK;
 }
 
+__global__ void adam_hyper_kernel(double* step, const double* lr, double beta1, double beta2, double wd,
+                                  const float* found_inf, float* hyper) {
+  if (threadIdx.x == 0) adam_hyper_update(step, lr, beta1, beta2, wd, found_inf, hyper);
+}
+
+int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, double wd,
+                   const float* found_inf, float* hyper, void* stream) {
+  hipLaunchKernelGGL(adam_hyper_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), step, lr,
+                     beta1, beta2, wd, found_inf, hyper);
+  HIP_RET(hipGetLastError());
+  return GS_OK;
+}
+
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
                       void* stream) {
   DeviceGuard g(p->device);
@@ -958,7 +1047,7 @@ int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, c
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     SgdOp<GS_OPT_N, GD, LD> op;
-    op.h = h; op.gscale = gsc; op.found_inf = fi;
+    op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
     return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;
@@ -969,7 +1058,7 @@ int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc,
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     AdamOp<GS_OPT_N, GD, LD> op;
-    op.h = h; op.gscale = gsc; op.found_inf = fi;
+    op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
     return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;

@@ -295,6 +295,16 @@ int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float
   return hip_clip_coef(sqnorm_dev, max_norm, eps, coef_dev, norm_dev, stream);
 }
 
+int gs_adam_hyper(int device_kind, double* step, const double* lr, double beta1, double beta2,
+                  double weight_decay, const float* found_inf, float* hyper, void* stream) {
+  GS_CHECK_ARG(step && lr && hyper, "gs_adam_hyper: NULL argument");
+  if (device_kind == GS_DEV_HOST) {
+    adam_hyper_update(step, lr, beta1, beta2, weight_decay, found_inf, hyper);
+    return GS_OK;
+  }
+  return hip_adam_hyper(step, lr, beta1, beta2, weight_decay, found_inf, hyper, stream);
+}
+
 int gs_unscale_check(gs_plan* p, int slot, int dtype, const float* inv_scale_dev,
                      float* found_inf_dev, void* stream) {
   PLAN_OK(p);
@@ -310,7 +320,8 @@ int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double mo
   PLAN_OK(p);
   GS_CHECK_ARG(!nesterov || (momentum > 0 && dampening == 0),
                "Nesterov momentum requires a momentum and zero dampening");
-  const SgdHyper h = make_sgd(lr, momentum, dampening, weight_decay, nesterov, maximize, first_step);
+  SgdHyper h = make_sgd(lr, momentum, dampening, weight_decay, nesterov, maximize, first_step);
+  if (p->kind == GS_DEV_HOST && p->hyper) h.lr = p->hyper[0];
   if (p->kind == GS_DEV_HOST) return host_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
   return hip_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
 }
@@ -321,10 +332,21 @@ int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double b
                  const float* found_inf_dev, void* stream) {
   PLAN_OK(p);
   GS_CHECK_ARG(bias_correction2_sqrt > 0, "gs_adam_step: bias_correction2_sqrt must be > 0");
-  const AdamHyper h = make_adam(lr, beta1, beta2, eps, weight_decay, adamw, maximize, step_size,
-                                bias_correction2_sqrt);
+  AdamHyper h = make_adam(lr, beta1, beta2, eps, weight_decay, adamw, maximize, step_size,
+                          bias_correction2_sqrt);
+  if (p->kind == GS_DEV_HOST && p->hyper) {
+    h.step_size = p->hyper[0];
+    h.bc2s = p->hyper[1];
+    h.decay = p->hyper[2];
+  }
   if (p->kind == GS_DEV_HOST) return host_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
   return hip_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
+}
+
+int gs_plan_set_hyper_source(gs_plan* p, const float* hyper) {
+  PLAN_OK(p);
+  p->hyper = hyper;
+  return GS_OK;
 }
 
 int gs_stream_wait(void* waiter, void* signaler) { return hip_stream_wait(waiter, signaler); }

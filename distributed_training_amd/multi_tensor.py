@@ -80,6 +80,20 @@ class TensorListPlan:
     def task_units(self) -> int:
         return int(L.lib().gs_plan_task_units(self.handle))
 
+    def set_hyper_source(self, hyper: torch.Tensor | None):
+        """Later sgd()/adam() launches read their step-varying hyper-parameters
+        from ``hyper`` (fp32, on the plan's device) when they run — SGD [lr];
+        Adam [step_size, bias_correction2_sqrt, 1 - lr*wd] — instead of their
+        arguments (gs_plan_set_hyper_source).  The plan keeps a reference."""
+        if hyper is not None:
+            if hyper.dtype != torch.float32 or not hyper.is_contiguous() or hyper.numel() < 3:
+                raise ValueError("hyper source: contiguous fp32 tensor of >= 3 elements")
+            if (hyper.device.type == "cuda") != (self.kind == L.GS_DEV_HIP):
+                raise ValueError("hyper source must live where the plan runs")
+        L.check(L.lib().gs_plan_set_hyper_source(self.handle, None if hyper is None else hyper.data_ptr()),
+                "gs_plan_set_hyper_source")
+        self._hyper = hyper
+
     def timer_enable(self, n_slots: int = 256):
         """Bracket every launch of this plan with HIP timing events on its
         launch stream (ring of n_slots); 0 disables."""

@@ -19,6 +19,15 @@ update multiplies grads by — clip coefficient or AMP 1/scale), ``found_inf``
 (skip the step when non-zero) and ``max_grad_norm`` (DeepSpeed-style
 ``gradient_clipping``: Σg² + coefficient computed on device, folded into the
 update kernel).
+
+``capturable=True`` (torch's Adam flag, also offered on SGD) makes ``step()``
+safe to record into a hipGraph (see :mod:`.graphs`): the step-varying
+hyper-parameters live in a small device buffer the update kernel reads when it
+runs (``gs_plan_set_hyper_source``) — SGD's lr; Adam's step_size, sqrt(bc2)
+and 1-lr·wd, produced on the device from a device step counter that does not
+advance on an AMP overflow (``gs_adam_hyper``, T:optim/adam.py capturable
+branch).  :meth:`refresh_hyper` copies a changed ``group["lr"]`` into that
+buffer outside the graph, so LR schedulers keep working across replays.
 """
 from __future__ import annotations
 
@@ -29,6 +38,11 @@ import torch
 
 from . import _lib as L
 from .multi_tensor import TensorListPlan, clip_coef, is_dense
+
+
+def _capturing() -> bool:
+    """Is torch's current stream recording a graph (False without a GPU)?"""
+    return torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()
 
 
 def _group_key(tensors):
@@ -70,6 +84,41 @@ class _FusedBase(torch.optim.Optimizer):
         self.grad_scale: torch.Tensor | None = None
         self.found_inf: torch.Tensor | None = None
         self._clip_buf: dict = {}
+        self._dev_hyper: dict = {}  # param-group index -> device hyper-parameter buffers
+
+    @property
+    def capturable(self) -> bool:
+        return bool(self.defaults.get("capturable"))
+
+    def _group_hyper(self, gi, group, device):
+        """Device buffers of group `gi` (capturable mode): ``hyper`` fp32[3]
+        read by the update kernel, ``lr`` fp64[1] (Adam's hyper producer)."""
+        h = self._dev_hyper.get(gi)
+        if h is None or h["hyper"].device != device:
+            if _capturing():
+                raise RuntimeError("capturable optimizer: take one step outside the graph before capturing it")
+            h = {"hyper": torch.zeros(3, dtype=torch.float32, device=device),
+                 "lr": torch.zeros(1, dtype=torch.float64, device=device), "lr_host": None}
+            self._dev_hyper[gi] = h
+        return h
+
+    def refresh_hyper(self):
+        """Write each group's host ``lr`` into its device buffer when it changed
+        (an eager fill, never recorded: call it outside a capture, before a
+        replay — graphs.CapturedStep does)."""
+        if _capturing():
+            return
+        for gi, group in enumerate(self.param_groups):
+            h = self._dev_hyper.get(gi)
+            if h is not None and h["lr_host"] != group["lr"]:
+                lr = float(group["lr"])
+                h["lr"].fill_(lr)
+                h["hyper"][0:1].fill_(lr)  # SGD reads hyper[0] = fp32(lr); Adam overwrites it
+                h["lr_host"] = group["lr"]
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev_hyper = {}  # device step counters are re-derived from the loaded state
 
     def enable_kernel_timer(self, n_slots: int = 256):
         """Time every update-kernel launch with HIP events recorded on its
@@ -119,7 +168,8 @@ class _FusedBase(torch.optim.Optimizer):
 
 class FusedSGD(_FusedBase):
     def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
-                 *, maximize=False, foreach=None, differentiable=False, fused=None, max_grad_norm=None):
+                 *, maximize=False, foreach=None, differentiable=False, fused=None, max_grad_norm=None,
+                 capturable=False):
         if lr < 0.0:
             raise ValueError(f"Invalid learning rate: {lr}")
         if momentum < 0.0:
@@ -132,7 +182,7 @@ class FusedSGD(_FusedBase):
             raise ValueError("FusedSGD does not support differentiable=True")
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                         nesterov=nesterov, maximize=maximize, foreach=foreach, differentiable=False,
-                        fused=fused, max_grad_norm=max_grad_norm)
+                        fused=fused, max_grad_norm=max_grad_norm, capturable=bool(capturable))
         super().__init__(params, defaults)
 
     def _collect(self, group):
@@ -167,16 +217,24 @@ class FusedSGD(_FusedBase):
                 loss = closure()
         new_bufs = any(group["momentum"] != 0 and p.grad is not None and "momentum_buffer" not in self.state[p]
                        for group in self.param_groups for p in group["params"])
+        if new_bufs and _capturing():
+            raise RuntimeError("FusedSGD: momentum buffers must exist before capture (take an eager step first)")
         if new_bufs and self._skipped_on_host():
             return loss
         work = []
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             for (gdt, first), (ps, gs, bs) in self._collect(group).items():
                 plan = self._plans.get(ps)
                 plan.set_ptrs(0, ps)
                 plan.set_ptrs(1, gs)
                 plan.set_ptrs(2, [b.data_ptr() if b is not None else 0 for b in bs])
+                if self.capturable:
+                    h = self._group_hyper(gi, group, ps[0].device)
+                    if getattr(plan, "_hyper", None) is not h["hyper"]:
+                        plan.set_hyper_source(h["hyper"])
                 work.append((group, plan, gdt, first))
+        if self.capturable:
+            self.refresh_hyper()
         if not work:
             return loss
         scale = self._clip_scale(work[0][1].device, [(w[1], w[2]) for w in work])
@@ -204,7 +262,7 @@ class FusedAdam(_FusedBase):
             raise ValueError("FusedAdam does not support differentiable=True")
         adamw = bool(decoupled_weight_decay if adamw is None else adamw)
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
-                        foreach=foreach, maximize=maximize, capturable=False, differentiable=False,
+                        foreach=foreach, maximize=maximize, capturable=bool(capturable), differentiable=False,
                         fused=fused, decoupled_weight_decay=adamw, max_grad_norm=max_grad_norm)
         super().__init__(params, defaults)
 
@@ -214,11 +272,14 @@ class FusedAdam(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if self._skipped_on_host():
+        cap = self.capturable
+        if not cap and self._skipped_on_host():
             return loss
         work = []
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             buckets = {}
+            h = None
+            start = len(work)
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -228,12 +289,25 @@ class FusedAdam(_FusedBase):
                 if p.dtype != torch.float32:
                     raise RuntimeError("FusedAdam expects fp32 parameters (keep a fp32 master copy)")
                 st = self.state[p]
-                if len(st) == 0:
+                if cap:
+                    if h is None:
+                        h = self._group_hyper(gi, group, p.device)
+                    if "step" not in h:  # one device counter per group, from the (loaded) state
+                        s0 = next((float(self.state[q]["step"]) for q in group["params"]
+                                   if "step" in self.state[q]), 0.0)
+                        h["step"] = torch.full((1,), s0, dtype=torch.float64, device=p.device)
+                if len(st) == 0 or "exp_avg" not in st:
+                    if _capturing():
+                        raise RuntimeError("FusedAdam: state must exist before capture (take an eager step first)")
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                key = (p.grad.dtype, float(st["step"].item()))
+                if cap:
+                    st["step"] = h["step"]  # shared device counter, advanced by gs_adam_hyper
+                    key = (p.grad.dtype, None)
+                else:
+                    st["step"] += 1
+                    key = (p.grad.dtype, float(st["step"].item()))
                 lists = buckets.setdefault(key, ([], [], [], []))
                 lists[0].append(p)
                 lists[1].append(p.grad)
@@ -245,12 +319,34 @@ class FusedAdam(_FusedBase):
                 plan.set_ptrs(1, gs)
                 plan.set_ptrs(2, ms)
                 plan.set_ptrs(3, vs)
+                if cap and getattr(plan, "_hyper", None) is not h["hyper"]:
+                    plan.set_hyper_source(h["hyper"])
                 work.append((group, plan, gdt, step))
+            if cap and h is not None:  # before the group's update launches
+                work.insert(start, (group, None, gi, h))
         if not work:
             return loss
-        scale = self._clip_scale(work[0][1].device, [(w[1], w[2]) for w in work])
+        if cap:
+            self.refresh_hyper()
+        plans = [(w[1], w[2]) for w in work if w[1] is not None]
+        if not plans:
+            return loss
+        scale = self._clip_scale(plans[0][0].device, plans)
         for group, plan, gdt, step in work:
             beta1, beta2 = group["betas"]
+            if plan is None:  # capturable: advance the group's device step, form its hyper source
+                h = step
+                L.check(L.lib().gs_adam_hyper(
+                    L.GS_DEV_HIP if h["step"].is_cuda else L.GS_DEV_HOST, h["step"].data_ptr(), h["lr"].data_ptr(),
+                    float(beta1), float(beta2), float(group["weight_decay"]),
+                    None if self.found_inf is None else self.found_inf.data_ptr(), h["hyper"].data_ptr(),
+                    L.stream_ptr(h["step"].device) if h["step"].is_cuda else None), "gs_adam_hyper")
+                continue
+            if step is None:  # the kernel reads step_size / bc2 / decay from the hyper source
+                plan.adam(gdt, group["lr"], beta1, beta2, group["eps"], group["weight_decay"],
+                          group["decoupled_weight_decay"], group["maximize"], -1.0, 1.0,
+                          grad_scale=scale, found_inf=self.found_inf)
+                continue
             lr = group["lr"]
             # python-double bias corrections, as torch's foreach path computes them
             bias_correction1 = 1 - beta1 ** step

@@ -104,6 +104,13 @@ int gs_comm_abort(gs_comm* c);
  * replaces: ProcessGroupNCCL's watchdog / TORCH_NCCL_ASYNC_ERROR_HANDLING
  *           (T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp:59-68, :156) */
 int gs_comm_set_timeout(gs_comm* c, int64_t timeout_ms);
+/* Pause (1) / resume (0) every communicator's watchdog event polling,
+ * process-wide and counted: bracket a global-mode hipGraph capture with it,
+ * since event queries from the watchdog thread are illegal while another
+ * thread records (collectives recorded into a graph are not tracked).
+ * replaces: ProcessGroupNCCL's capture-time watchdog exclusion
+ *           (T:.../c10d/ProcessGroupNCCL.cpp, "graph capture" handling) */
+int gs_watchdog_pause(int pause);
 /* 1 if aborted (reason copied into `reason`, NUL-terminated), 0 if live */
 int gs_comm_status(gs_comm* c, char* reason, int cap);
 int gs_comm_rank(gs_comm* c);
@@ -223,6 +230,24 @@ int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double b
                  double beta2, double eps, double weight_decay, int adamw, int maximize,
                  double step_size, double bias_correction2_sqrt, const float* grad_scale_dev,
                  const float* found_inf_dev, void* stream);
+/* Step-varying hyper-parameters from memory instead of the arguments: with a
+ * non-NULL source, every later gs_sgd_step / gs_adam_step on this plan reads
+ *   SGD:  hyper[0] = lr
+ *   Adam: hyper[0] = step_size (-lr/bc1), hyper[1] = bias_correction2_sqrt,
+ *         hyper[2] = 1 - lr*wd (AdamW decay)
+ * (fp32, device memory for HIP plans, host memory for host plans) when the
+ * kernel runs, so a step recorded into a hipGraph follows an LR schedule and
+ * Adam's bias corrections on replay; the argument values are then ignored.
+ * NULL restores argument hyper-parameters.  The buffer must outlive its use.
+ * replaces: T:optim/adam.py capturable=True (device step / tensor lr) */
+int gs_plan_set_hyper_source(gs_plan* p, const float* hyper);
+/* Adam hyper source update on the stream (one thread; graph-capturable):
+ *   if (!found_inf || *found_inf == 0) *step += 1;
+ *   hyper = [-(lr/bc1), sqrt(bc2), 1 - lr*wd]  with bcK = 1 - betaK^step, in double
+ * step, lr: fp64 scalars; hyper: fp32[3] (the plan's hyper source).
+ * replaces: T:optim/adam.py:640-668 (capturable branch: device step, bias corrections) */
+int gs_adam_hyper(int device_kind, double* step, const double* lr, double beta1, double beta2,
+                  double weight_decay, const float* found_inf, float* hyper, void* stream);
 
 /* ======================================================================
  * bucket assignment (greedy by size per dtype, first-bucket cap)

@@ -1,0 +1,149 @@
+"""hipGraph capture of libgsync launches and of the whole DDP training step.
+
+* plan tables under capture: a recorded launch replays against the pointers
+  it was recorded with, even after eager launches re-pointed the plan;
+* device hyper-parameter source: a recorded SGD / Adam step follows an LR
+  change and Adam's bias corrections across replays, equal to eager steps;
+* CapturedStep over DDP (ws 1, RCCL collective recorded) + capturable FusedSGD
+  / FusedAdam: weights track an eager twin through warmup, capture, replays
+  and an LR schedule.
+"""
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests._dist_util import free_port, init_pg
+
+pytestmark = pytest.mark.gpu
+
+
+def test_recorded_pack_keeps_its_pointers(cuda_device):
+    from distributed_training_amd.multi_tensor import TensorListPlan
+
+    shapes = [1000, 37, 70000, 5]
+    a = [torch.randn(n, device=cuda_device) for n in shapes]
+    b = [torch.randn(n, device=cuda_device) for n in shapes]
+    plan = TensorListPlan(shapes, cuda_device)
+    flat = torch.zeros(plan.flat_numel, device=cuda_device)
+    plan.set_ptrs(0, a)
+    plan.pack(0, torch.float32, flat)  # eager launch first (table upload path)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        plan.pack(0, torch.float32, flat, 2.0, 1)  # recorded against a
+    plan.set_ptrs(0, b)
+    plan.pack(0, torch.float32, flat)  # eager against b
+    torch.cuda.synchronize()
+    assert torch.equal(flat[: sum(shapes)], torch.cat(b))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(flat[: sum(shapes)], torch.cat(a) * 2.0)
+    plan.pack(0, torch.float32, flat)  # eager again: the plan re-uploads b's table
+    torch.cuda.synchronize()
+    assert torch.equal(flat[: sum(shapes)], torch.cat(b))
+
+
+def _opt_pair(cls, cuda_device, **kw):
+    torch.manual_seed(0)
+    shapes = [(64, 3, 3, 3), (64,), (10, 512), (7,)]
+    p_e = [torch.randn(s, device=cuda_device) for s in shapes]
+    p_g = [p.clone() for p in p_e]
+    return p_e, p_g, cls(p_e, capturable=False, **kw), cls(p_g, capturable=True, **kw)
+
+
+@pytest.mark.parametrize("which", ["sgd", "adam", "adamw"])
+def test_recorded_optimizer_step_follows_lr_and_bias_correction(cuda_device, which):
+    import distributed_training_amd as D
+
+    if which == "sgd":
+        p_e, p_g, oe, og = _opt_pair(D.FusedSGD, cuda_device, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        p_e, p_g, oe, og = _opt_pair(D.FusedAdam, cuda_device, lr=1e-2, weight_decay=0.01, adamw=which == "adamw")
+    gen = torch.Generator(device=cuda_device).manual_seed(3)
+    grads = [[torch.randn(p.shape, device=cuda_device, generator=gen) for p in p_e] for _ in range(6)]
+    static = [torch.zeros_like(p) for p in p_g]
+    for p, s in zip(p_g, static):
+        p.grad = s
+    graph = None
+    for it in range(6):
+        if it == 4:
+            for o in (oe, og):
+                o.param_groups[0]["lr"] *= 0.3
+        for p, gr in zip(p_e, grads[it]):
+            p.grad = gr.clone()
+        oe.step()
+        for s, gr in zip(static, grads[it]):
+            s.copy_(gr)
+        if it < 2:
+            og.step()  # eager warmup creates state
+            continue
+        if graph is None:
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                og.step()
+        og.refresh_hyper()
+        graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(p_e, p_g):
+        torch.testing.assert_close(b, a, rtol=0, atol=1e-6)
+
+
+@pytest.fixture(scope="module")
+def rccl_pg(cuda_device):
+    if dist.is_initialized():
+        yield
+        return
+    init_pg("nccl", 0, 1, free_port())
+    yield
+    from distributed_training_amd.comm import destroy_communicators
+
+    destroy_communicators()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_captured_ddp_step_tracks_eager(cuda_device, rccl_pg, opt_name):
+    import torch.nn as nn
+
+    import distributed_training_amd as D
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    runs = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = micro_resnet().to(cuda_device).to(memory_format=torch.channels_last)
+        ddp = D.DistributedDataParallel(model)
+        if opt_name == "sgd":
+            opt = D.FusedSGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4, capturable=True)
+        else:
+            opt = D.FusedAdam(ddp.parameters(), lr=1e-3, capturable=True)
+        crit = nn.CrossEntropyLoss()
+
+        def train_step(x, y):
+            opt.zero_grad(set_to_none=False)
+            loss = crit(ddp(x), y)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        step = D.CapturedStep(train_step, optimizers=[opt], warmup=3) if mode == "graph" else train_step
+        gen = torch.Generator(device=cuda_device).manual_seed(1)
+        losses = []
+        for it in range(8):
+            if it == 6:
+                opt.param_groups[0]["lr"] *= 0.5  # scheduler: read from device on replay
+            x = torch.rand(16, 3, 32, 32, device=cuda_device, generator=gen).to(memory_format=torch.channels_last)
+            y = torch.randint(0, 10, (16,), device=cuda_device, generator=gen)
+            losses.append(float(step(x, y)))
+        torch.cuda.synchronize()
+        if mode == "graph":
+            assert step.captures == 1 and step.replays == 5
+        runs[mode] = ([p.detach().clone() for p in model.parameters()], losses)
+        del ddp, opt
+    (pe, le), (pg, lg) = runs["eager"], runs["graph"]
+    assert all(abs(a - b) <= 1e-3 * max(1.0, abs(a)) for a, b in zip(le, lg)), (le, lg)
+    for a, b in zip(pe, pg):
+        torch.testing.assert_close(b, a, rtol=1e-3, atol=1e-4)
