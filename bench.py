@@ -67,6 +67,12 @@ def parse():
                          "(-1: only when N > 1)")
     ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: N>1 control-flow rehearsal with ranks sharing GPUs (not a measurement)")
+    ap.add_argument("--impl", default="libgsync", choices=["libgsync", "torch"],
+                    help="torch = the reference path on the same GPU (torch DDP + torch.optim SGD/Adam foreach), "
+                         "for comparison; DDP engine only")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: record the whole step (forward, backward + bucket sync, update) into one hipGraph "
+                         "(CapturedStep, capturable optimizer) and replay it")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -167,14 +173,28 @@ def main():
     bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
     n_params = sum(p.numel() for p in model.parameters())
     zero = None
-    if args.engine == "ddp":
+    if args.impl == "torch":
+        if args.engine != "ddp" or args.graph:
+            raise SystemExit("--impl torch: DDP engine, eager only")
+        ddp = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[dev.index] if args.pg_backend == "nccl" else None,
+            bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=args.grad_as_bucket_view)
+        if args.optimizer == "sgd":
+            opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=True)
+            bytes_per_param = 20
+        else:
+            opt = torch.optim.Adam(ddp.parameters(), lr=1e-3 * world, foreach=True)
+            bytes_per_param = 28
+        grad_bytes = n_params * 4
+    elif args.engine == "ddp":
         ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
                                         gradient_as_bucket_view=args.grad_as_bucket_view)
         if args.optimizer == "sgd":
-            opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+            opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4,
+                             capturable=bool(args.graph))
             bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
         else:
-            opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world)
+            opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world, capturable=bool(args.graph))
             bytes_per_param = 28
         grad_bytes = n_params * (2 if bucket_dtype is not None else 4)
     else:
@@ -213,13 +233,25 @@ def main():
             if i is not None:
                 ev_opt[i][1].record()
             return loss
+        return run(x, y)
+
+    def train_step(xb, yb):
+        if args.graph:
+            opt.zero_grad(set_to_none=False)  # recorded grads are reused across replays
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = ddp(x)
-            loss = crit(out, y)
+            out = ddp(xb)
+            loss = crit(out, yb)
         loss.backward()
         opt.step()
-        opt.zero_grad(set_to_none=True)
+        if not args.graph:
+            opt.zero_grad(set_to_none=True)
         return loss
+
+    run = train_step
+    if args.graph:
+        if zero is not None:
+            raise SystemExit("--graph: DDP engine only")
+        run = D.CapturedStep(train_step, optimizers=[opt], warmup=max(1, args.warmup - 1))
 
     t_w0 = time.time()
     for i in range(args.warmup):
@@ -231,7 +263,9 @@ def main():
     warm_s = time.time() - t_w0
 
     comm_ms = []
-    if zero is None:
+    if args.impl == "torch":
+        pass
+    elif zero is None:
         opt.enable_kernel_timer(args.steps + 4)
     else:
         zero.plan.timer_enable(4 * args.steps + 8)  # + the Σg² launches of the clip
@@ -246,14 +280,24 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.pg_backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    if zero is None:
-        comm_ms = ddp.bucket_comm_ms()  # last iteration, per bucket (HIP events on the comm stream)
+    if zero is None and args.impl == "libgsync":
+        comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # last iteration, per bucket (HIP events on the comm stream)
 
     coll = None
-    if args.collective_bench == 1 or (args.collective_bench == -1 and world > 1):
+    if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
         coll = collective_bench(ddp, zero, world)
 
-    if zero is None:
+    if args.impl == "torch":
+        opt_ms = []
+    elif zero is None and args.graph:
+        # replays carry no timing events: time the update kernel over a few eager
+        # launches on the same state after the timed region (same kernel, same plan)
+        opt.enable_kernel_timer(8)
+        for _ in range(5):
+            opt.step()
+        torch.cuda.synchronize()
+        opt_ms = sorted(opt.kernel_ms())
+    elif zero is None:
         # update-kernel launches, HIP events recorded by libgsync on the launch stream
         # right around each kernel (the pointer-table upload, if any, stays outside)
         opt_ms = sorted(opt.kernel_ms())
@@ -264,7 +308,7 @@ def main():
 
         opt_ms = sorted(zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM))
         win_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
-    opt_ms_avg = sum(opt_ms) / len(opt_ms)
+    opt_ms_avg = sum(opt_ms) / len(opt_ms) if opt_ms else None
     img_s = world * args.batch * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
 
@@ -273,7 +317,7 @@ def main():
         return
 
     upd_params = n_params if zero is None else n_params // world  # ZeRO updates this rank's shard
-    achieved = bytes_per_param * upd_params / (opt_ms_avg * 1e-3) / 1e9
+    achieved = bytes_per_param * upd_params / (opt_ms_avg * 1e-3) / 1e9 if opt_ms_avg else None
     traffic = None
     if os.path.exists(args.traffic_json) and zero is None:
         try:
@@ -283,7 +327,10 @@ def main():
             traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    if zero is None:
+    if args.impl == "torch":
+        log = ddp._get_ddp_logging_data()
+        bucket_bytes = [int(b) for b in str(log.get("rebuilt_bucket_sizes", "")).split(",") if b.strip()]
+    elif zero is None:
         log = ddp._get_ddp_logging_data()
         bucket_bytes = [b.numel() * b.element_size() for b in ddp._bucketer.buffers]
     else:
@@ -317,7 +364,10 @@ def main():
         "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
         "config": {
             "workload": (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
-                         f"libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
+                         f"REFERENCE PATH torch DDP + torch.optim.{'SGD' if args.optimizer == 'sgd' else 'Adam'}"
+                         f"(foreach) for comparison") if args.impl == "torch" else
+                        (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+                         f"{'one hipGraph per step: ' if args.graph else ''}libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
                          f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}") if zero is None else
                         (f"{args.model} synthetic 224x224 bf16 model training, {args.batch} img/GPU, libgsync "
                          f"{args.engine.upper()} (bf16 {'reduce-scatter' if args.engine == 'zero2' else 'all-reduce'}"
@@ -331,11 +381,13 @@ def main():
             "bucket_dtype": args.bucket_dtype,
             "channels_last": not args.no_channels_last,
             "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
+            "impl": args.impl,
+            "hipgraph": bool(args.graph),
             **({"rehearsal": "gloo, ranks sharing GPUs: control flow only, not a measurement"}
                if args.pg_backend == "gloo" else {}),
             "params": n_params,
         },
-        "roofline": {
+        "roofline": None if args.impl == "torch" else {
             "kernel": (f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
                        if zero is None else
                        f"gs ZeRO shard update (mt_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> + bf16 param write)"),
@@ -343,18 +395,19 @@ def main():
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS,
+            "frac": achieved / HBM_PEAK_GBPS if achieved else None,
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
             "avg_launch_ms": opt_ms_avg,
             "launches": len(opt_ms),
-            "timing": "libgsync plan launch timer: HIP events recorded on the launch stream around each kernel",
-            "median_launch_ms": opt_ms[len(opt_ms) // 2],
+            "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
+                       + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")),
+            "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
         },
         "grad_sync": grad_sync,
         **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
         "warmup_s": warm_s,
-        "has_rebuilt_buckets": log["has_rebuilt_buckets"],
+        "has_rebuilt_buckets": log.get("has_rebuilt_buckets", 0),
     }
     if args.cpu_baseline and world == 1:
         from oracle.cpu_ddp_baseline import run as cpu_run
