@@ -1,0 +1,76 @@
+"""bench.py's output contract on the GPU, at a small size (ResNet-18, 16 images).
+
+* N=1: one JSON line on stdout with the driver's keys, a `roofline` object for
+  the fused update kernel and a `grad_sync` object; the process exits 0.
+* N=2 through `torch.distributed.run` exactly as the driver launches it, with
+  `--pg-backend gloo` (RCCL refuses two ranks on one GPU): barriers, the MAX
+  over ranks and the rank-0-only line — the control flow of the driver's
+  N = 2/4/8 runs, not a measurement.
+
+The benches run as child processes (never exec'd from this process)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--model", "resnet18", "--batch", "16", "--steps", "3", "--warmup", "2", "--cpu-baseline", "0"]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check_line(d, n):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "grad_sync"):
+        assert k in d, k
+    assert d["n_gpus"] == n and d["steps"] == 3 and d["warmup"] == 2
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["config"]["workload"] and d["config"]["parallelism"] == f"dp{n}"
+    assert d["config"]["global_batch"] == 16 * n
+    # value = all ranks' images / the (max-over-ranks) timed region
+    assert abs(d["value"] - n * 16 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["achieved"] > 0 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert r["algorithmic_bytes_per_launch"] == 20 * d["config"]["params"]
+    assert r["launches"] == 3
+    g = d["grad_sync"]
+    assert g["n_buckets"] == len(g["bucket_bytes"]) >= 1
+    assert g["grad_bytes_per_step"] == 4 * d["config"]["params"]
+
+
+def test_bench_n1_contract(cuda_device):
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL, cwd=REPO,
+                       capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]
+    _check_line(lines[0], 1)
+    assert lines[0]["config"]["impl"] == "libgsync"
+
+
+def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "bench.py", "--gpus", "2", "--pg-backend", "gloo"] + SMALL
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=500)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    _check_line(lines[0], 2)
+    assert "rehearsal" in lines[0]["config"]
