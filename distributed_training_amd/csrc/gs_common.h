@@ -55,10 +55,13 @@ constexpr int kMinTaskUnits = 256;        // one unit per lane of a 256-thread w
 #ifndef GS_TARGET_TASKS
 #define GS_TARGET_TASKS 1920
 #endif
-constexpr int kTargetTasks = GS_TARGET_TASKS;  // < kMaxGrid: ragged tensor ends add tasks
+constexpr int kTargetTasks = GS_TARGET_TASKS;  // < 2048 resident: ragged tensor ends add tasks
 constexpr int kMaxSegPerTask = 64;
 constexpr int kBlock = 256;         // 4 waves of 64
-constexpr int kMaxGrid = 2048;      // 256 CUs x 8 workgroups (default grid cap)
+// default grid: one workgroup per task up to kGridLimit (the dispatcher refills
+// CUs faster than a resident grid loops: profiles/r1r_copy_micro.jsonl,
+// r1r_grid_sweep.jsonl); GS_MAX_GRID=2048 restores the one-resident-wave cap
+constexpr int kMaxGrid = 65536;
 constexpr int kGridLimit = 65536;   // hard cap (partials buffer); GS_MAX_GRID env for tuning
 
 struct Seg {

@@ -41,8 +41,8 @@ gs::PlanArgs gs_plan::args() const {
   return a;
 }
 
-// Task size (units) of a plan.  Every task is one workgroup's work; the grid
-// holds at most kMaxGrid = 256 CUs x 8 resident workgroups.  Plans up to
+// Task size (units) of a plan.  Every task is one workgroup's work; 256 CUs
+// hold 2048 resident workgroups (256 CUs x 8).  Plans up to
 // ~1920 x 16 Ki elements are cut into ~kTargetTasks tasks: one wave of
 // workgroups evenly spread over the CUs (no second partial round), rounded to
 // whole 256-lane iterations.  Larger plans keep 16 Ki-element tasks
@@ -50,6 +50,10 @@ gs::PlanArgs gs_plan::args() const {
 // puts 64 Ki-element tasks 20-25 % below 8-16 Ki-element ones on pack/unpack
 // of 120 M-element plans, while a second round of tasks costs little there.
 // GS_TASK_UNITS=<n> / GS_TARGET_TASKS=<n> in the environment override (tuning runs).
+// Optimizer-update plans ask for 512-unit tasks instead (gs_plan_create_ex,
+// multi_tensor.UPDATE_TASK_UNITS): five streams per element make the
+// per-task descriptor prologue cheap relative to the data, and a short task
+// per workgroup streams +2-8 % faster (profiles/r1r_grid_sweep.jsonl).
 int64_t plan_task_units(int64_t total_units) {
   static const int64_t forced = [] {
     const char* e = std::getenv("GS_TASK_UNITS");

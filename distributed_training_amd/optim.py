@@ -37,7 +37,7 @@ from typing import Iterable
 import torch
 
 from . import _lib as L
-from .multi_tensor import TensorListPlan, clip_coef, is_dense
+from .multi_tensor import TensorListPlan, clip_coef, is_dense, update_task_units
 
 
 def _capturing() -> bool:
@@ -60,7 +60,8 @@ class _PlanCache:
         key = tuple(id(p) for p in params) + (params[0].device,)
         plan = self._plans.get(key)
         if plan is None:
-            plan = TensorListPlan([p.numel() for p in params], params[0].device)
+            plan = TensorListPlan([p.numel() for p in params], params[0].device,
+                                  task_units=update_task_units(params[0].device))
             if self.timer_slots and plan.kind == L.GS_DEV_HIP:
                 plan.timer_enable(self.timer_slots)
             self._plans[key] = plan

@@ -36,7 +36,7 @@ import torch.distributed as dist
 from . import _lib as L
 from .comm import get_communicator
 from .ddp import BUCKET_ALIGN_ELEMS, compute_bucket_assignment_by_size
-from .multi_tensor import TensorListPlan, clip_coef, dense_like_param
+from .multi_tensor import TensorListPlan, clip_coef, dense_like_param, update_task_units
 
 
 class DynamicLossScaler:
@@ -206,7 +206,7 @@ class ZeroDataParallel:
             self.master = self.param_shards  # fp32 model: the shard IS the master copy
         self.state1 = [torch.zeros(s, dtype=torch.float32, device=self.device) for s in shard_sizes]
         self.state2 = [torch.zeros(s, dtype=torch.float32, device=self.device) for s in shard_sizes]
-        self.plan = TensorListPlan(shard_sizes, self.device)
+        self.plan = TensorListPlan(shard_sizes, self.device, task_units=update_task_units(self.device))
         self.plan.set_ptrs(0, self.master)
         self.plan.set_ptrs(1, self.grad_shards)
         self.plan.set_ptrs(2, self.state1)

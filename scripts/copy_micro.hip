@@ -1,0 +1,109 @@
+// Streaming scale-copy shapes at the grad-sync sizes, to locate the gap between
+// libgsync's pack (one resident wave of looping workgroups) and HIP's own D2D
+// copy at Infinity-Cache-resident sizes (profiles/r1n_ab_interleave_ceiling.jsonl:
+// 4.8 vs 6.7 TB/s at 25.6 M fp32).  Not product code.
+//   hipcc -O3 --offload-arch=gfx950 scripts/copy_micro.hip -o scripts/build/copy_micro
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                     \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return 1;                                                                   \
+    }                                                                             \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kB = 256;
+
+// one shot: K float4 per lane, no loop, grid covers the array
+template <int K>
+__global__ void __launch_bounds__(kB) copy_grid(const f4* __restrict__ s, f4* __restrict__ d, long n4, float a) {
+  const long base = static_cast<long>(blockIdx.x) * kB * K + threadIdx.x;
+  f4 v[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const long i = base + j * kB;
+    if (i < n4) v[j] = s[i];
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const long i = base + j * kB;
+    if (i < n4) d[i] = v[j] * a;
+  }
+}
+
+// resident grid, chunks of kB*ILP float4 taken round-robin (the interleaved sweep)
+template <int ILP>
+__global__ void __launch_bounds__(kB) copy_persist(const f4* __restrict__ s, f4* __restrict__ d, long n4, float a) {
+  for (long c = blockIdx.x; c * kB * ILP < n4; c += gridDim.x) {
+    const long base = c * kB * ILP + threadIdx.x;
+    f4 v[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const long i = base + j * kB;
+      if (i < n4) v[j] = s[i];
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const long i = base + j * kB;
+      if (i < n4) d[i] = v[j] * a;
+    }
+  }
+}
+
+template <class F>
+static float timed(F f, hipEvent_t* ev, int reps) {
+  for (int i = 0; i < 5; ++i) f();
+  std::vector<float> ms(reps);
+  for (int i = 0; i < reps; ++i) {
+    (void)hipEventRecord(ev[0], 0);
+    f();
+    (void)hipEventRecord(ev[1], 0);
+    (void)hipEventSynchronize(ev[1]);
+    (void)hipEventElapsedTime(&ms[i], ev[0], ev[1]);
+  }
+  std::sort(ms.begin(), ms.end());
+  return ms[reps / 2];
+}
+
+int main() {
+  const long sizes[] = {25557032L, 60192808L, 120385616L};
+  hipEvent_t ev[2];
+  CK(hipEventCreate(&ev[0]));
+  CK(hipEventCreate(&ev[1]));
+  for (long n : sizes) {
+    const long n4 = n / 4;
+    const size_t bytes = static_cast<size_t>(n4) * 16;
+    f4 *s, *d;
+    CK(hipMalloc(&s, bytes));
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemset(s, 0, bytes));
+    CK(hipMemset(d, 0, bytes));
+    const double alg = 2.0 * bytes;
+    auto rate = [&](float ms) { return alg / (ms * 1e-3) / 1e9; };
+    printf("{\"elements\": %ld, \"bytes\": %.0f", n, alg);
+    float t = timed([&] { (void)hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, 0); }, ev, 30);
+    printf(", \"hipMemcpy_D2D\": %.0f", rate(t));
+#define GRID(K)                                                                                         \
+  t = timed([&] { copy_grid<K><<<(n4 + kB * K - 1) / (kB * K), kB>>>(s, d, n4, 0.5f); }, ev, 30); \
+  printf(", \"grid_k%d\": %.0f", K, rate(t));
+    GRID(1) GRID(2) GRID(4) GRID(8)
+#define PERSIST(ILP, G)                                                              \
+  t = timed([&] { copy_persist<ILP><<<G, kB>>>(s, d, n4, 0.5f); }, ev, 30); \
+  printf(", \"persist_ilp%d_g%d\": %.0f", ILP, G, rate(t));
+    PERSIST(4, 1024) PERSIST(4, 1920) PERSIST(4, 2048) PERSIST(4, 4096) PERSIST(2, 2048) PERSIST(2, 4096)
+    PERSIST(1, 8192)
+    CK(hipGetLastError());
+    printf("}\n");
+    fflush(stdout);
+    CK(hipFree(s));
+    CK(hipFree(d));
+  }
+  return 0;
+}

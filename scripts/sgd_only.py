@@ -8,7 +8,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from distributed_training_amd.multi_tensor import TensorListPlan  # noqa: E402
+from distributed_training_amd.multi_tensor import TensorListPlan, update_task_units  # noqa: E402
 from distributed_training_amd.resnet import MODELS  # noqa: E402
 
 model = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
@@ -20,7 +20,7 @@ ps = [torch.randn(s, device=dev) for s in shapes]
 gs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
 bs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
 vs = [torch.rand(s, device=dev) * 1e-4 for s in shapes] if op == "adam" else None
-plan = TensorListPlan([p.numel() for p in ps], dev)
+plan = TensorListPlan([p.numel() for p in ps], dev, task_units=update_task_units(dev))  # as FusedSGD/FusedAdam
 for k, ts in enumerate((ps, gs, bs) + ((vs,) if vs is not None else ())):
     plan.set_ptrs(k, ts)
 for _ in range(iters):

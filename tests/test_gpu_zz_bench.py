@@ -7,7 +7,8 @@
   over ranks and the rank-0-only line — the control flow of the driver's
   N = 2/4/8 runs, not a measurement.
 
-The benches run as child processes (never exec'd from this process)."""
+The benches run as child processes (never exec'd from this process); the
+module is named to run after the other GPU modules."""
 import json
 import os
 import socket
@@ -26,6 +27,17 @@ def _port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _env():
+    """A clean rendezvous for the child: earlier test modules leave this
+    process's own MASTER_PORT / RANK / WORLD_SIZE in os.environ (and the port
+    still bound by their process group)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env["MASTER_PORT"] = str(_port())
+    return env
 
 
 def _json_lines(out):
@@ -54,7 +66,7 @@ def _check_line(d, n):
 
 
 def test_bench_n1_contract(cuda_device):
-    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL, cwd=REPO,
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL, cwd=REPO, env=_env(),
                        capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
@@ -64,7 +76,7 @@ def test_bench_n1_contract(cuda_device):
 
 
 def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = _env()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            "bench.py", "--gpus", "2", "--pg-backend", "gloo"] + SMALL
