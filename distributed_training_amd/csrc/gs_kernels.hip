@@ -447,7 +447,10 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
   return static_cast<char*>(flat) + off * (DT == GS_F32 ? 4 : 2);
 }
 
-template <int N, int SD, int FD>
+// MODE (GS_SCALE_NONE / _MUL / _DIV) is a template parameter: a runtime mode
+// left a uniform branch and the unused IEEE-division path inside every
+// lane-step of the streaming loop
+template <int N, int SD, int FD, int MODE>
 struct PackOp {
   static constexpr int kN = N;
   static constexpr int kRed = 0;
@@ -457,7 +460,6 @@ struct PackOp {
   void* flat;
   bool flat_vec;
   float s;
-  int mode;
   struct Frag { float x[N]; };
   __device__ bool active() const { return true; }
   __device__ void load(const TV& v, int64_t e, Frag& f) const {
@@ -472,9 +474,9 @@ struct PackOp {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       float x = f.x[i];
-      if (mode == GS_SCALE_MUL) {
+      if constexpr (MODE == GS_SCALE_MUL) {
         x = x * s;
-      } else if (mode == GS_SCALE_DIV) {
+      } else if constexpr (MODE == GS_SCALE_DIV) {
         // bf16_compress_hook order: round to the bucket dtype, then divide
         x = round_to<FD>(x) / s;
       }
@@ -955,13 +957,23 @@ int hip_plan_flush(gs_plan* p, void* stream) {
     default: return fail(GS_EINVAL, "unsupported low-precision dtype");  \
   }
 
+template <int SD, int FD, int MODE>
+static int pack_mode(gs_plan* p, int src_slot, void* flat, float s, void* stream) {
+  PackOp<GS_PACK_N, SD, FD, MODE> op;
+  op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s;
+  return launch<GS_PACK_ILP>(p, op, stream);
+}
+
 int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
              void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(src_dt, SD, GS_DISPATCH_FLOAT(flat_dt, FD, {
-    PackOp<GS_PACK_N, SD, FD> op;
-    op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s; op.mode = mode;
-    return launch<GS_PACK_ILP>(p, op, stream);
+    switch (mode) {
+      case GS_SCALE_NONE: return pack_mode<SD, FD, GS_SCALE_NONE>(p, src_slot, flat, s, stream);
+      case GS_SCALE_MUL: return pack_mode<SD, FD, GS_SCALE_MUL>(p, src_slot, flat, s, stream);
+      case GS_SCALE_DIV: return pack_mode<SD, FD, GS_SCALE_DIV>(p, src_slot, flat, s, stream);
+      default: return fail(GS_EINVAL, "gs_pack: unknown scale mode");
+    }
   }));
   return GS_OK;
 }
