@@ -99,6 +99,10 @@ def main():
     sq = torch.zeros(1, device=dev)
     rec("unpack_f32+sqnorm", 8 * n, *timeit_plan(plan, lambda: plan.unpack(flat, 2, torch.float32, sqnorm=sq), args.iters), "libgsync")
     rec("sqnorm_f32", 4 * n, *timeit_plan(plan, lambda: plan.sqnorm(1, torch.float32, sq), args.iters), "libgsync")
+    # the update kernels run on an update plan, as FusedSGD / FusedAdam build it
+    from distributed_training_amd.multi_tensor import update_task_units
+
+    plan = TensorListPlan([torch.Size(s).numel() for s in shapes], dev, task_units=update_task_units(dev))
     plan.set_ptrs(0, params)
     plan.set_ptrs(1, grads)
     plan.set_ptrs(2, bufs)
