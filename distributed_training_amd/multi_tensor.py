@@ -10,6 +10,7 @@ gradient-sync path.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Sequence
 
 import torch
@@ -23,7 +24,7 @@ from . import _lib as L
 # one-resident-wave tasking: fused SGD +8 % on ResNet-50, +2 % on ResNet-152,
 # Adam +1-3 % (profiles/r1r_grid_sweep.jsonl).  Pack / unpack keep the default
 # sizing (short tasks cost them 20-50 % there).
-UPDATE_TASK_UNITS = 512
+UPDATE_TASK_UNITS = int(os.environ.get("GSYNC_UPDATE_TASK_UNITS", "512"))  # 0 = library default (A/B runs)
 
 
 def update_task_units(device) -> int:
