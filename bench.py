@@ -73,6 +73,13 @@ def parse():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: record the whole step (forward, backward + bucket sync, update) into one hipGraph "
                          "(CapturedStep, capturable optimizer) and replay it")
+    ap.add_argument("--bucket-policy", default="torch", choices=["torch", "xgmi"],
+                    help="DDP bucket caps: torch's (default, torch-parity layout) or from the live all-reduce "
+                         "curve at N>1 (distributed_training_amd.ddp.xgmi_bucket_caps)")
+    ap.add_argument("--last-bucket-cap-mb", type=float, default=None,
+                    help="cap the last bucket in gradient-ready order (the exposed end-of-backward chain)")
+    ap.add_argument("--parity", type=int, default=1,
+                    help="after the timed region: one self-checked step (distributed_training_amd.parity)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -188,7 +195,8 @@ def main():
         grad_bytes = n_params * 4
     elif args.engine == "ddp":
         ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
-                                        gradient_as_bucket_view=args.grad_as_bucket_view)
+                                        gradient_as_bucket_view=args.grad_as_bucket_view,
+                                        bucket_policy=args.bucket_policy, last_bucket_cap_mb=args.last_bucket_cap_mb)
         if args.optimizer == "sgd":
             opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4,
                              capturable=bool(args.graph))
@@ -280,12 +288,40 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.pg_backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
+    tail = timeline = None
     if zero is None and args.impl == "libgsync":
         comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # last iteration, per bucket (HIP events on the comm stream)
+        if not args.graph:
+            tail = ddp.tail_ms()  # last timed step: last bucket ready -> all bucket chains done
+            timeline = ddp.bucket_timeline_ms()
 
     coll = None
     if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
         coll = collective_bench(ddp, zero, world)
+
+    parity = None
+    if args.parity and args.impl == "libgsync" and not args.graph:
+        from distributed_training_amd import parity as PC
+
+        if zero is None:
+            def fwd_bwd():
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = crit(ddp(x), y)
+                loss.backward()
+
+            opt_ms_saved = opt.kernel_ms()  # the timed launches, read before the check step adds one
+            parity = PC.ddp_parity_step(ddp, opt, fwd_bwd)
+            opt.kernel_ms()
+        else:
+            def fwd_bwd():
+                crit(ddp(x).float(), y).backward()
+
+            from distributed_training_amd import _lib as L
+
+            zero_ms_saved = zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM)
+            parity = PC.zero_parity_step(zero, fwd_bwd)
+        if rank == 0:
+            print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
 
     if args.impl == "torch":
         opt_ms = []
@@ -300,13 +336,14 @@ def main():
     elif zero is None:
         # update-kernel launches, HIP events recorded by libgsync on the launch stream
         # right around each kernel (the pointer-table upload, if any, stays outside)
-        opt_ms = sorted(opt.kernel_ms())
+        opt_ms = sorted(opt_ms_saved if parity is not None else opt.kernel_ms())
     else:
         # the fused shard update alone (plan launch timer); the whole zero.step() window
         # (norm, clip, update, all-gather) is reported beside it
         from distributed_training_amd import _lib as L
 
-        opt_ms = sorted(zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM))
+        opt_ms = sorted(zero_ms_saved if parity is not None else
+                        zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM))
         win_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
     opt_ms_avg = sum(opt_ms) / len(opt_ms) if opt_ms else None
     img_s = world * args.batch * args.steps / elapsed
@@ -349,8 +386,16 @@ def main():
                                   "last timed step, includes cross-rank arrival skew under backward"})
     if coll is not None:
         grad_sync["standalone"] = coll
+    if tail is not None:
+        grad_sync["tail_ms"] = tail
+        grad_sync["bucket_timeline_ms"] = timeline
+    if zero is None and args.impl == "libgsync":
+        grad_sync["bucket_policy"] = log.get("bucket_policy")
+        if log.get("xgmi_calibration"):
+            grad_sync["xgmi_calibration"] = log["xgmi_calibration"]
+    model_label = {"resnet18": "ResNet-18", "resnet50": "ResNet-50", "resnet152": "ResNet-152"}[args.model]
     line = {
-        "metric": "images/sec (node) ResNet-50 at 1/2/4/8 MI355X; grad-sync bus GB/s",
+        "metric": f"images/sec (node) {model_label} at 1/2/4/8 MI355X; grad-sync bus GB/s",
         "value": img_s,
         "unit": "images/sec",
         "n_gpus": world,
@@ -405,24 +450,34 @@ def main():
             "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
         },
         "grad_sync": grad_sync,
+        "parity": parity,
         **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
         "warmup_s": warm_s,
         "has_rebuilt_buckets": log.get("has_rebuilt_buckets", 0),
     }
     if args.cpu_baseline and world == 1:
-        from oracle.cpu_ddp_baseline import run as cpu_run
+        from oracle.cpu_ddp_baseline import cpu_model_name, run as cpu_run
 
         cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        cb = cpu_run(model=args.model, batch=16, ws=2, cores=cores, steps=3, warmup=1, port=_free_port())
+        # leg 1 (the headline unit): the reference's torch-DDP/gloo path on this workload's model at 224x224;
+        # leg 2: BASELINE configs[0], the reference's own workload (ResNet-18 CIFAR, 100 img/rank, ws=2)
+        cb = cpu_run(model=args.model, batch=16, ws=2, cores=cores, steps=5, warmup=1, port=_free_port())
+        c1 = cpu_run(model="resnet18", batch=100, ws=2, cores=cores, steps=10, warmup=2, port=_free_port())
         line["cpu_baseline"] = {
             "value": cb["images_per_sec"],
             "unit": "images/sec",
             "cores": cb["cores"],
+            "cpu_model": cpu_model_name(),
             "kind": "port",
             "gloo_allreduce_busbw_GBps": cb["gloo_allreduce_busbw_GBps"],
             "gloo_allreduce_bytes": cb["gloo_allreduce_bytes"],
             "sample": f"torch DDP+gloo {args.model} 224x224, Adam(lr=1e-3*ws), ws=2 x 16 img/rank, "
-                      f"1 warmup + 3 timed steps (restates R:resnet/pytorch_ddp/ddp_train.py:79-114 on CPU)",
+                      f"1 warmup + 5 timed steps (restates R:resnet/pytorch_ddp/ddp_train.py:79-114 on CPU)",
+            "config0_resnet18_cifar": {
+                "value": c1["images_per_sec"], "unit": "images/sec", "cores": c1["cores"],
+                "gloo_allreduce_busbw_GBps": c1["gloo_allreduce_busbw_GBps"],
+                "sample": "torch DDP+gloo resnet18 32x32 10 classes, Adam(lr=1e-3*ws), ws=2 x 100 img/rank "
+                          "(R:resnet/pytorch_ddp/ddp_train.py:95,97,110-111), 2 warmup + 10 timed steps"},
         }
     print(json.dumps(line), flush=True)
     dist.destroy_process_group()

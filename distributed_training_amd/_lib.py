@@ -135,6 +135,7 @@ SIGNATURES = {
     "gs_bucketer_unpack_bucket": (_c_int, [_vp, _c_int, _vp]),
     "gs_bucketer_set_found_inf": (_c_int, [_vp, _vp]),
     "gs_bucketer_last_comm_ms": (_c_int, [_vp, _c_int, _p_f]),
+    "gs_bucketer_last_timing": (_c_int, [_vp, _c_int, _p_f]),
 }
 
 

@@ -6,7 +6,10 @@ growth 2.0 every 2000 clean steps, backoff 0.5) but replaces
 ``_amp_foreach_non_finite_check_and_unscale_`` (:280) with one libgsync
 multi-tensor pass, and for libgsync fused optimizers folds the 1/scale into
 the update kernel and skips the step ON THE DEVICE when a non-finite grad was
-found — no host synchronisation per step.  Reached from the Colossal
+found: SGD's first-step flag and Adam's step counter live on the device and
+advance only on a clean step, so a scale/backward/step/update iteration does
+no host synchronisation (tests/test_gpu_amp_nosync.py).  Foreign optimizers
+keep torch's host read of the flag (T:amp/grad_scaler.py _maybe_opt_step).  Reached from the Colossal
 ``torch_ddp_fp16`` plugin (R:resnet/colossal/colossal_train.py:129-130).
 """
 from __future__ import annotations
@@ -63,7 +66,9 @@ class GradScaler:
         if not self._enabled:
             return outputs
         self._lazy_init(outputs.device)
-        return outputs * self._scale.to(outputs.dtype)
+        # as torch: the fp32 scale multiplies without a cast (an fp16 loss is
+        # promoted to fp32 — the default 2**16 does not fit fp16)
+        return outputs * self._scale.to(device=outputs.device, non_blocking=True)
 
     def get_scale(self):
         return self._init_scale if self._scale is None else float(self._scale.item())
@@ -90,7 +95,9 @@ class GradScaler:
         st["inv_scale"].copy_(self._scale.reciprocal())
         st["found_inf"].zero_()
         for dt, grads in self._grads(optimizer).items():
-            key = (id(optimizer), dt, tuple(id(g) for g in grads))
+            # a plan depends only on the sizes and the device (grads are
+            # short-lived: ids are reused after zero_grad(set_to_none))
+            key = (id(optimizer), dt, grads[0].device, tuple(g.numel() for g in grads))
             plan = self._plans.get(key)
             if plan is None:
                 plan = TensorListPlan([g.numel() for g in grads], grads[0].device)

@@ -248,6 +248,11 @@ class Booster:
     def boost(self, model, optimizer=None, criterion=None, dataloader=None, lr_scheduler=None):
         model, optimizer = self.plugin.configure(model, optimizer, self.mixed_precision)
         self._zero = optimizer.zero if isinstance(optimizer, _ZeroOptimizerWrapper) else None
+        amp = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(self.mixed_precision)
+        if criterion is not None and amp is not None and isinstance(self.plugin, TorchDDPPlugin):
+            # Colossal's FP16TorchMixedPrecision.configure wraps the criterion in
+            # the autocast module too: the loss is computed in fp32 under autocast
+            criterion = _AutocastModule(criterion, amp)
         return model, optimizer, criterion, dataloader, lr_scheduler
 
     def backward(self, loss, optimizer):

@@ -52,7 +52,9 @@ struct Bucket {
   int pending = 0;
   bool launched = false;
   bool unpacked = false;
-  hipEvent_t ev_ready = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+  // timing (all on the comm stream but ev_ready, recorded on the producer):
+  // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
+  hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
   bool timed = false;
 };
 
@@ -79,6 +81,7 @@ struct gs_bucketer {
   float* found_inf = nullptr;  // AMP non-finite flag of the averaged grads (fused into unpack)
   void* producer = nullptr;
   hipEvent_t ev_done = nullptr;
+  bool done_timed = false;
   std::mutex mu;
 
   bool hip() const { return kind == GS_DEV_HIP; }
@@ -168,14 +171,16 @@ int launch_bucket(gs_bucketer* b, int bi) {
     hipStream_t cs = comm_stream(b->comm);
     HIPB_RET(hipEventRecord(bk.ev_ready, static_cast<hipStream_t>(b->producer)));
     HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
-    GS_TRY_RET(pack_one(b, bk, cs));
     // timing events stay out of a hipGraph capture (last_comm_ms then reports -1)
     const bool timed = !stream_capturing(cs);
+    if (timed) HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
+    GS_TRY_RET(pack_one(b, bk, cs));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_t0, cs));
     GS_TRY_RET(launch_collective(b, bk, cs));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
     bk.timed = timed;
     if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
+    if (timed) HIPB_RET(hipEventRecord(bk.ev_u1, cs));
   } else {
     GS_TRY_RET(pack_one(b, bk, b->producer));
   }
@@ -261,16 +266,16 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     if (rc != GS_OK) return bail(rc);
     bk.pending = static_cast<int>(bk.params.size());
     if (device_kind == GS_DEV_HIP) {
-      if (hipEventCreateWithFlags(&bk.ev_ready, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess)
+      if (hipEventCreate(&bk.ev_ready) != hipSuccess || hipEventCreate(&bk.ev_pk0) != hipSuccess ||
+          hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess ||
+          hipEventCreate(&bk.ev_u1) != hipSuccess)
         return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
     }
   }
   for (int p = 0; p < n_params; ++p)
     if (b->loc_bucket[p] < 0)
       return bail(fail(GS_EINVAL, "gs_bucketer_create: parameter " + std::to_string(p) + " is in no bucket"));
-  if (device_kind == GS_DEV_HIP &&
-      hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming) != hipSuccess)
+  if (device_kind == GS_DEV_HIP && hipEventCreate(&b->ev_done) != hipSuccess)
     return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
   *out = b;
   return GS_OK;
@@ -282,9 +287,8 @@ int gs_bucketer_destroy(gs_bucketer* b) {
   for (Bucket& bk : b->buckets) {
     gs_plan_destroy(bk.plan);
     gs_plan_destroy(bk.flat);
-    if (bk.ev_ready) (void)hipEventDestroy(bk.ev_ready);
-    if (bk.ev_t0) (void)hipEventDestroy(bk.ev_t0);
-    if (bk.ev_t1) (void)hipEventDestroy(bk.ev_t1);
+    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1})
+      if (ev) (void)hipEventDestroy(ev);
   }
   if (b->ev_done) (void)hipEventDestroy(b->ev_done);
   delete b;
@@ -395,6 +399,7 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
   if (b->hip() && b->auto_coll()) {
     hipStream_t cs = comm_stream(b->comm);
     HIPB_RET(hipEventRecord(b->ev_done, cs));
+    b->done_timed = !stream_capturing(cs);
     HIPB_RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), b->ev_done, 0));
   } else if (b->do_unpack() || b->found_inf) {
     for (Bucket& bk : b->buckets)
@@ -419,6 +424,23 @@ int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream) {
   Bucket& bk = b->buckets[bucket];
   if (!bk.launched) return fail(GS_ESTATE, "unpack of a bucket that was never launched");
   return unpack_one(b, bk, stream, 0);
+}
+
+int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out) {
+  GS_CHECK_ARG(b && out && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  for (int i = 0; i < 5; ++i) out[i] = -1.f;
+  Bucket& bk = b->buckets[bucket];
+  if (!bk.timed || !b->hip() || !b->auto_coll()) return GS_OK;
+  HIPB_RET(hipEventSynchronize(bk.ev_u1));
+  HIPB_RET(hipEventElapsedTime(&out[0], bk.ev_ready, bk.ev_pk0));
+  HIPB_RET(hipEventElapsedTime(&out[1], bk.ev_pk0, bk.ev_t0));
+  HIPB_RET(hipEventElapsedTime(&out[2], bk.ev_t0, bk.ev_t1));
+  HIPB_RET(hipEventElapsedTime(&out[3], bk.ev_t1, bk.ev_u1));
+  if (b->done_timed) {
+    HIPB_RET(hipEventSynchronize(b->ev_done));
+    HIPB_RET(hipEventElapsedTime(&out[4], bk.ev_ready, b->ev_done));
+  }
+  return GS_OK;
 }
 
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms) {

@@ -73,6 +73,26 @@ struct Seg {
 };
 static_assert(sizeof(Seg) == 24, "Seg layout");
 
+// ---- chunk-map engine (streaming ops) ----
+// The plan's tensors are laid end to end in a VIRTUAL element space (voff):
+// a tensor of >= kGroupElems elements starts on a kGroupElems boundary, one of
+// >= kChunkElems on a kChunkElems boundary, a smaller one on a 4-element
+// boundary.  The space is cut into chunks of kChunkElems (one 16-B access per
+// lane of a 256-lane workgroup); a workgroup takes G consecutive chunks per
+// iteration (G per op, gs_kernels.hip) and grid-strides.  A group of chunks
+// that lies wholly inside one tensor is streamed with no per-lane lookup and
+// no bounds checks: a wave-uniform base pointer (SGPRs) plus a 32-bit lane
+// offset, G accesses per stream in flight; the rest (tensor tails, runs of
+// small tensors) go chunk by chunk, resolving each lane's tensor by binary
+// search over voff.
+constexpr int kChunkElems = 256 * kUnit;    // 1 Ki elements
+constexpr int kGroupElems = 4 * kChunkElems;  // largest group (G = 4)
+struct ChunkDesc {
+  int32_t t0;    // first tensor intersecting the chunk
+  int32_t code;  // 0: full chunk inside t0; k > 0: k tensors intersect; -1: empty
+};
+static_assert(sizeof(ChunkDesc) == 8, "ChunkDesc layout");
+
 // Arguments handed to a device kernel (by value).
 struct PlanArgs {
   const Seg* segs;
@@ -81,8 +101,15 @@ struct PlanArgs {
   const int64_t* off;         // [n] flat offsets (elements)
   void* const* ptrs;          // [GS_PLAN_SLOTS * n]
   const uint32_t* align;      // [n] bit s = slot s pointer is 16-B aligned
+  const ChunkDesc* chunks;    // [n_chunks]
+  const int64_t* voff;        // [n] virtual offsets (chunk-map engine)
+  uint32_t* ticket;           // arrival counter of the fused reduction (0 between launches)
+  float* red_out;             // fused reduction target (chunk engine), NULL = none
+  int32_t red_acc;            // accumulate into red_out
+  int32_t per_wg;             // chunk engine: groups per workgroup (0 = grid-stride)
   int32_t n;
   int32_t n_tasks;
+  int32_t n_chunks;
 };
 
 // optimizer hyper-parameters, rounded to fp32 where torch rounds them
@@ -119,14 +146,17 @@ struct gs_plan {
   std::vector<int64_t> numel, off;
   std::vector<gs::Seg> segs;
   std::vector<int32_t> task_begin;
+  std::vector<int64_t> voff;           // chunk-map engine: virtual offsets
+  std::vector<gs::ChunkDesc> chunks;   // chunk-map engine: one per kChunkElems elements of voff space
   int grid = 0;
+  int grid_cap = gs::kMaxGrid;         // GS_MAX_GRID
   int64_t task_units = 0;
   // host shadow of the pointer table
   std::vector<void*> h_ptrs;       // [SLOTS * n]
   std::vector<uint32_t> h_align;   // [n]
   bool dirty = true;
   // device side (HIP plans only)
-  void* d_static = nullptr;  // segs | task_begin | numel | off
+  void* d_static = nullptr;  // segs | task_begin | numel | off | chunks | voff | ticket
   void* d_table = nullptr;   // ptrs | align
   float* d_partials = nullptr;  // [kGridLimit]
   void* pinned = nullptr;       // staging ring for table uploads

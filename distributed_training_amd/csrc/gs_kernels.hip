@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 
 #include "gs_common.h"
 
@@ -115,6 +116,29 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #endif
 #ifndef GS_OPT_N
 #define GS_OPT_N 4
+#endif
+// chunks per workgroup iteration (chunk-map engine), per op; measured in
+// profiles/r2*_kernels_*.jsonl (scripts/r2_engine_ab.sh)
+#ifndef GS_FUSED_RED
+#define GS_FUSED_RED 0  // 1: chunk-engine reductions combine in-kernel (ticket) — measured slower (r2c)
+#endif
+#ifndef GS_G_PACK
+#define GS_G_PACK 1     // fp32 bucket
+#endif
+#ifndef GS_G_PACK16
+#define GS_G_PACK16 2   // 16-bit bucket
+#endif
+#ifndef GS_G_UNPACK
+#define GS_G_UNPACK 2
+#endif
+#ifndef GS_G_RED
+#define GS_G_RED 2
+#endif
+#ifndef GS_G_SGD
+#define GS_G_SGD 2
+#endif
+#ifndef GS_G_ADAM
+#define GS_G_ADAM 4
 #endif
 // 256-thread workgroups are admitted 8 per CU only while the kernel uses <= 80
 // SGPRs (MI355X_MICROARCH.md, residency); cap the allocation there
@@ -229,6 +253,63 @@ __device__ __forceinline__ void storeN(void* base, int64_t e, int64_t n, bool ve
   }
 }
 
+// Full-chunk access of the chunk-map engine: `base` is wave-uniform (SGPRs),
+// e0 the uniform element index of the chunk inside the tensor and `lo` the
+// lane's 32-bit element offset; everything is in range and 16-B aligned, so
+// the access is one global_load/store with an SGPR base and a VGPR offset.
+template <int DT>
+__device__ __forceinline__ const void* elem_at(const void* base, int64_t e0) {
+  return static_cast<const char*>(base) + e0 * (DT == GS_F32 ? 4 : 2);
+}
+template <int DT>
+__device__ __forceinline__ void load4F(const void* base, uint32_t lo, float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    const gf4 v = vload((const GLOBAL_AS gf4*)(gptr<float>(base) + lo));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+    const gu2 v = vload((const GLOBAL_AS gu2*)(gptr<uint16_t>(base) + lo));
+    x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
+    x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
+    x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
+    x[3] = to_f32<DT>(static_cast<uint16_t>(v.y >> 16));
+  }
+}
+template <int DT>
+__device__ __forceinline__ void store4F(void* base, uint32_t lo, const float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    gf4 v;
+    v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
+    vstore((GLOBAL_AS gf4*)(gptr_w<float>(base) + lo), v);
+  } else {
+    gu2 v;
+    v.x = static_cast<uint32_t>(from_f32<DT>(x[0])) | (static_cast<uint32_t>(from_f32<DT>(x[1])) << 16);
+    v.y = static_cast<uint32_t>(from_f32<DT>(x[2])) | (static_cast<uint32_t>(from_f32<DT>(x[3])) << 16);
+    vstore((GLOBAL_AS gu2*)(gptr_w<uint16_t>(base) + lo), v);
+  }
+}
+// F = full-chunk fast path (above); otherwise element e0 + lo of a tensor of
+// n elements with the bounds / alignment checks of loadN / storeN
+template <int DT, int N, bool F>
+__device__ __forceinline__ void ld(const void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
+                                   float (&x)[N]) {
+  if constexpr (F) {
+    static_assert(N == 4, "the chunk engine moves 4 elements per lane-access");
+    load4F<DT>(elem_at<DT>(base, e0), lo, x);
+  } else {
+    loadN<DT, N>(base, e0 + lo, n, vec, x);
+  }
+}
+template <int DT, int N, bool F>
+__device__ __forceinline__ void st(void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
+                                   const float (&x)[N]) {
+  if constexpr (F) {
+    static_assert(N == 4, "the chunk engine moves 4 elements per lane-access");
+    store4F<DT>(const_cast<void*>(elem_at<DT>(base, e0)), lo, x);
+  } else {
+    storeN<DT, N>(base, e0 + lo, n, vec, x);
+  }
+}
+
 __device__ __forceinline__ void* slot_ptr(const PlanArgs& P, int slot, int t) {
   return P.ptrs[static_cast<int64_t>(slot) * P.n + t];
 }
@@ -305,12 +386,12 @@ __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const in
 #pragma unroll
       for (int j = 0; j < ILP; ++j) {
         const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-        if (u < total) op.load(v, (ub + u) * kUnit, f[j]);
+        if (u < total) op.template load<false>(v, (ub + u) * kUnit, 0u, f[j]);
       }
 #pragma unroll
       for (int j = 0; j < ILP; ++j) {
         const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-        if (u < total) op.apply(v, (ub + u) * kUnit, f[j], acc);
+        if (u < total) op.template apply<false>(v, (ub + u) * kUnit, 0u, f[j], acc);
       }
     }
     return;
@@ -332,12 +413,12 @@ __device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const in
         }
         kk[j] = lo;
         ee[j] = (s_ubeg[lo] + (u - s_pref[lo])) * kUnit;
-        op.load(s_tv[lo], ee[j], f[j]);
+        op.template load<false>(s_tv[lo], ee[j], 0u, f[j]);
       }
     }
 #pragma unroll
     for (int j = 0; j < ILP; ++j)
-      if (kk[j] >= 0) op.apply(s_tv[kk[j]], ee[j], f[j], acc);
+      if (kk[j] >= 0) op.template apply<false>(s_tv[kk[j]], ee[j], 0u, f[j], acc);
   }
 }
 
@@ -353,12 +434,12 @@ __device__ __forceinline__ void run_interleaved(const Op& op, const TV& v, int p
 #pragma unroll
     for (int j = 0; j < ILP; ++j) {
       const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-      if (u < total) op.load(v, static_cast<int64_t>(u) * kUnit, f[j]);
+      if (u < total) op.template load<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j]);
     }
 #pragma unroll
     for (int j = 0; j < ILP; ++j) {
       const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-      if (u < total) op.apply(v, static_cast<int64_t>(u) * kUnit, f[j], acc);
+      if (u < total) op.template apply<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j], acc);
     }
   }
 }
@@ -371,6 +452,30 @@ __device__ __forceinline__ void run_interleaved(const Op& op, const TV& v, int p
 template <class T>
 __device__ __forceinline__ T cload(const T* p, int64_t i) {
   return ((const CONST_AS T*)(p))[i];
+}
+
+// Descriptor of tensor t as `op` addresses it: logical slot k is table row
+// op.phys(k), so single-stream ops read their runtime slot as the constant
+// logical slot 0.  (A runtime index into TV::ptr made the compiler spill the
+// descriptor to scratch and reload the stream pointer into VGPRs, turning
+// every access into per-lane 64-bit addressing.)  SCALAR: wave-uniform t,
+// loaded through the constant address space (s_load).
+template <bool SCALAR, class Op>
+__device__ __forceinline__ TV load_tv(const Op& op, const PlanArgs& P, int t) {
+  TV v;
+  const uint32_t a = SCALAR ? cload(P.align, t) : P.align[t];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int s = 0; s < GS_PLAN_SLOTS; ++s) {
+    const int64_t r = static_cast<int64_t>(op.phys(s)) * P.n + t;
+    v.ptr[s] = SCALAR ? cload(P.ptrs, r) : P.ptrs[r];
+    bits |= ((a >> op.phys(s)) & 1u) << s;
+  }
+  v.align = bits;
+  v.numel = SCALAR ? cload(P.numel, t) : P.numel[t];
+  v.off = SCALAR ? cload(P.off, t) : P.off[t];
+  v.pad = 0;
+  return v;
 }
 
 template <int ILP, class Op>
@@ -391,13 +496,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
       const int64_t ub = q->unit_begin;
       const int units = q->units;
       const int parts = q->pad;
-      TV v;
-#pragma unroll
-      for (int s = 0; s < GS_PLAN_SLOTS; ++s) v.ptr[s] = cload(P.ptrs, static_cast<int64_t>(s) * P.n + t);
-      v.numel = cload(P.numel, t);
-      v.off = cload(P.off, t);
-      v.align = cload(P.align, t);
-      v.pad = 0;
+      const TV v = load_tv<true>(op, P, t);
       if (parts > 0) run_interleaved<ILP>(op, v, static_cast<int>(ub), parts, units, acc);
       else run_units<ILP>(op, &v, &ub, nullptr, 1, units, acc);
       continue;
@@ -405,14 +504,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
     if (threadIdx.x < ns) {
       const Seg sg = P.segs[sb + threadIdx.x];
       const int t = sg.tensor;
-      TV v;
-#pragma unroll
-      for (int s = 0; s < GS_PLAN_SLOTS; ++s) v.ptr[s] = P.ptrs[static_cast<int64_t>(s) * P.n + t];
-      v.numel = P.numel[t];
-      v.off = P.off[t];
-      v.align = P.align[t];
-      v.pad = 0;
-      s_tv[threadIdx.x] = v;
+      s_tv[threadIdx.x] = load_tv<false>(op, P, t);
       s_ubeg[threadIdx.x] = sg.unit_begin;
       s_pref[threadIdx.x] = sg.task_off;
       if (threadIdx.x == ns - 1) s_pref[ns] = sg.task_off + sg.units;
@@ -427,18 +519,193 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
   }
 }
 
-// deterministic combine of the per-workgroup partials (fixed order)
+// deterministic combine of the per-workgroup partials (fixed order): 1024
+// threads, thread t folds partials t, t+1024, ... in that order with 16 loads
+// issued before the first add, then a fixed-tree block reduction
+constexpr int kCombineBlock = 1024;
 template <bool MAX>
-__global__ void __launch_bounds__(kBlock) combine_partials(const float* partials, int n,
-                                                           float* out, int accumulate) {
+__global__ void __launch_bounds__(kCombineBlock) combine_partials(const float* partials, int n,
+                                                                  float* out, int accumulate) {
+  __shared__ float s_red[kCombineBlock / 64];
   float v = 0.f;
-  for (int i = threadIdx.x; i < n; i += kBlock)
-    v = MAX ? fmaxf(v, partials[i]) : v + partials[i];
-  const float r = block_reduce<MAX>(v);
+  for (int i = threadIdx.x; i < n; i += 16 * kCombineBlock) {
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = (i + u * kCombineBlock < n) ? partials[i + u * kCombineBlock] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (i + u * kCombineBlock < n) v = MAX ? fmaxf(v, x[u]) : v + x[u];
+  }
+  v = MAX ? wave_max(v) : wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
   if (threadIdx.x == 0) {
+    float r = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kCombineBlock / 64; ++w) r = MAX ? fmaxf(r, s_red[w]) : r + s_red[w];
     if (MAX) out[0] = accumulate ? fmaxf(out[0], r) : r;
     else out[0] = accumulate ? out[0] + r : r;
   }
+}
+
+// ------------------------------------------------------- chunk-map engine
+// (layout: gs_common.h).  A workgroup takes G consecutive 1 Ki-element chunks
+// per iteration and grid-strides.  A group wholly inside one tensor whose
+// streams are all 16-B aligned runs the op's F = true path: the descriptor
+// comes through scalar loads and every lane issues G 16-B accesses per stream
+// (SGPR base + 32-bit VGPR offset) before the first use, with no bounds or
+// alignment branches.  Other groups go chunk by chunk: a full chunk the same
+// way with one access per lane, a mixed chunk (tensor tails, runs of small
+// tensors) by a per-lane binary search over voff and the checked path.
+// Reductions write one partial per workgroup; the grid is capped for them so
+// that the combine reads few partials (combine_partials, fixed order).
+template <class Op>
+__device__ __forceinline__ void chunk_mixed(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
+                                            float& acc) {
+  const int64_t e = c * kChunkElems + static_cast<int>(threadIdx.x) * kUnit;
+  int lo = t0, hi = t0 + span - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P.voff[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  const int64_t local = e - P.voff[lo];
+  if (local < 0 || local >= P.numel[lo]) return;  // alignment gap between tensors
+  const TV v = load_tv<false>(op, P, lo);
+  typename Op::Frag f;
+  op.template load<false>(v, local, 0u, f);
+  op.template apply<false>(v, local, 0u, f, acc);
+}
+
+template <int G, class Op>
+__device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int t, int64_t c0, float& acc) {
+  // G chunks c0 .. c0+G-1, all inside tensor t
+  const TV v = load_tv<true>(op, P, t);
+  const int64_t e0 = c0 * kChunkElems - cload(P.voff, t);
+  const uint32_t tid = threadIdx.x;
+  typename Op::Frag f[G];
+  if (op.fast_ok(v)) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template apply<true>(v, e0, j * kChunkElems + tid * kUnit, f[j], acc);
+  } else {
+    // a stream is not 16-B aligned: the checked path over the same range
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template load<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template apply<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j], acc);
+  }
+}
+
+template <class Op>
+__global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, Op op) {
+  static_assert(Op::kN == kUnit, "the chunk engine moves 4 elements per lane-access");
+  constexpr int G = Op::kG;
+  static_assert(G == 1 || G == 2 || G == 4, "group of 1, 2 or 4 chunks");
+  float acc = 0.f;
+  if (!op.active()) return;  // uniform across the grid
+  load_hyper(op);            // uniform: graph-replayable lr / bias corrections
+  const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
+  const int* cw = &P.chunks[0].t0;  // [t0, code] pairs
+  // groups per workgroup: grid-stride (per_wg == 0) or a contiguous range
+  const int64_t g_begin = P.per_wg ? blockIdx.x * static_cast<int64_t>(P.per_wg) : blockIdx.x;
+  const int64_t g_end = P.per_wg ? std::min<int64_t>(n_groups, g_begin + P.per_wg) : n_groups;
+  const int64_t g_step = P.per_wg ? 1 : gridDim.x;
+  for (int64_t g = g_begin; g < g_end; g += g_step) {
+    const int64_t c0 = g * G;
+    const int t = cload(cw, 2 * c0);
+    const int code = cload(cw, 2 * c0 + 1);
+    if constexpr (G > 1) {
+      // the whole group inside one tensor: first and last chunk full in t
+      if (code == 0 && c0 + G <= P.n_chunks && cload(cw, 2 * (c0 + G - 1)) == t &&
+          cload(cw, 2 * (c0 + G - 1) + 1) == 0) {
+        chunk_full<G>(op, P, t, c0, acc);
+        continue;
+      }
+    }
+    for (int j = 0; j < G; ++j) {
+      const int64_t c = c0 + j;
+      if (c >= P.n_chunks) break;
+      const int tj = j == 0 ? t : cload(cw, 2 * c);
+      const int cj = j == 0 ? code : cload(cw, 2 * c + 1);
+      if (cj == 0) chunk_full<1>(op, P, tj, c, acc);
+      else if (cj > 0) chunk_mixed(op, P, tj, cj, c, acc);
+    }
+  }
+  if constexpr (Op::kRed != 0) {
+    constexpr bool MAX = Op::kRed == 2;
+    const float r = block_reduce<MAX>(acc);
+#if GS_FUSED_RED
+    // fused combine: the partial goes out write-through (agent-scope store),
+    // then the workgroup arrives on a device-scope ticket; the last to arrive
+    // reads every partial with agent-scope loads (L2-served, never a stale
+    // L1 line), combines them in combine_partials' fixed order and re-arms
+    // the ticket.  No release/acquire fences: MI355X_MICROARCH.md hand-off
+    // table, row 1 (sc1 stores, s_waitcnt vmcnt(0), atomic add, sc1 loads).
+    if (P.red_out == nullptr) return;  // uniform
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&op.partials[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(P.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = tk == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      float v = 0.f;
+      for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += kBlock) {
+        const float x = __hip_atomic_load(&op.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = MAX ? fmaxf(v, x) : v + x;
+      }
+      const float tot = block_reduce<MAX>(v);
+      if (threadIdx.x == 0) {
+        float* out = P.red_out;
+        if (MAX) out[0] = P.red_acc ? fmaxf(out[0], tot) : tot;
+        else out[0] = P.red_acc ? out[0] + tot : tot;
+        __hip_atomic_store(P.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#else
+    if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+#endif
+  }
+}
+
+// Which ops stream through the chunk-map engine (bit 1 << GS_OP_*); the rest
+// use the task engine.  GS_ENGINE=<mask> overrides (A/B runs).
+#ifndef GS_CHUNK_OPS
+#define GS_CHUNK_OPS 254
+#endif
+bool use_chunk_engine(int kind) {
+  static const int mask = [] {
+    const char* e = std::getenv("GS_ENGINE");
+    return e ? std::atoi(e) : GS_CHUNK_OPS;
+  }();
+  return (mask >> kind) & 1;
+}
+// reductions: at most this many workgroups (= partials for the combine),
+// each taking a contiguous range of groups (GS_RED_CONTIG=1) or grid-striding;
+// GS_RED_GRID / GS_RED_CONTIG in the environment override (sweeps)
+#ifndef GS_RED_GRID
+#define GS_RED_GRID 2048
+#endif
+#ifndef GS_RED_CONTIG
+#define GS_RED_CONTIG 0
+#endif
+int red_grid_cap() {
+  static const int v = [] {
+    const char* e = std::getenv("GS_RED_GRID");
+    const int x = e ? std::atoi(e) : GS_RED_GRID;
+    return std::max(1, std::min(x, kGridLimit));
+  }();
+  return v;
+}
+bool red_contiguous() {
+  static const bool v = [] {
+    const char* e = std::getenv("GS_RED_CONTIG");
+    return e ? std::atoi(e) != 0 : GS_RED_CONTIG != 0;
+  }();
+  return v;
 }
 
 // ---------------------------------------------------------------- ops
@@ -447,12 +714,19 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
   return static_cast<char*>(flat) + off * (DT == GS_F32 ? 4 : 2);
 }
 
+// Op access convention: load<F> / apply<F>(tv, e0, lo, frag[, acc]) handle the
+// 4 (or kN) elements starting at element e0 + lo of tensor tv.  F = true is
+// the chunk engine's full-chunk path (e0 wave-uniform, no bounds checks, every
+// stream 16-B aligned: `fast_ok` says when a tensor qualifies); F = false is
+// the general path with bounds / alignment checks (lo = 0 there).
+
 // MODE (GS_SCALE_NONE / _MUL / _DIV) is a template parameter: a runtime mode
 // left a uniform branch and the unused IEEE-division path inside every
 // lane-step of the streaming loop
 template <int N, int SD, int FD, int MODE>
 struct PackOp {
   static constexpr int kN = N;
+  static constexpr int kG = FD == GS_F32 ? GS_G_PACK : GS_G_PACK16;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_PACK;
   float* partials = nullptr;
@@ -461,16 +735,23 @@ struct PackOp {
   bool flat_vec;
   float s;
   struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
   __device__ bool active() const { return true; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    const void* src = v.ptr[slot];
+  __device__ bool fast_ok(const TV& v) const {
+    return flat_vec && (v.off % 4) == 0 && (v.ptr[0] == nullptr || v.vec(0));
+  }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    const void* src = v.ptr[0];
     if (src == nullptr) {  // unused parameter (find_unused_parameters): pack zeros
       for (int i = 0; i < N; ++i) f.x[i] = 0.f;
       return;
     }
-    loadN<SD, N>(src, e, v.numel, v.vec(slot), f.x);
+    ld<SD, N, F>(src, e0, lo, v.numel, v.vec(0), f.x);
   }
-  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       float x = f.x[i];
@@ -482,7 +763,7 @@ struct PackOp {
       }
       f.x[i] = x;
     }
-    storeN<FD, N>(flat_at<FD>(flat, v.off), e, v.numel, flat_vec && (v.off % N) == 0, f.x);
+    st<FD, N, F>(flat_at<FD>(flat, v.off), e0, lo, v.numel, flat_vec && (v.off % N) == 0, f.x);
   }
 };
 
@@ -491,6 +772,7 @@ struct PackOp {
 template <int N, int FD, int DD, int RED = 1>
 struct UnpackOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = RED;
   static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
@@ -499,21 +781,28 @@ struct UnpackOp {
   bool flat_vec;
   int slot;
   struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
   __device__ bool active() const { return true; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    loadN<FD, N>(flat_at<FD>(const_cast<void*>(flat), v.off), e, v.numel,
-              flat_vec && (v.off % N) == 0, f.x);
+  __device__ bool fast_ok(const TV& v) const {
+    return flat_vec && (v.off % 4) == 0 && (v.ptr[0] == nullptr || v.vec(0));
   }
-  __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
-    void* dst = v.ptr[slot];
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<FD, N, F>(flat_at<FD>(const_cast<void*>(flat), v.off), e0, lo, v.numel,
+                 flat_vec && (v.off % N) == 0, f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float& acc) const {
+    void* dst = v.ptr[0];
     if (dst == nullptr) return;  // unused parameter: grad left untouched
-    storeN<DD, N>(dst, e, v.numel, v.vec(slot), f.x);
+    st<DD, N, F>(dst, e0, lo, v.numel, v.vec(0), f.x);
     if (want_red) {
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         const float r = round_to<DD>(f.x[i]);
         if constexpr (RED == 1) acc = fmaf(r, r, acc);
-        else if (e + i < v.numel && !isfinite(r)) acc = 1.f;
+        else if ((F || e0 + lo + i < v.numel) && !isfinite(r)) acc = 1.f;
       }
     }
   }
@@ -522,6 +811,7 @@ struct UnpackOp {
 template <int N, int DT>
 struct ScaleOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_SCALE;
   float* partials = nullptr;
@@ -529,30 +819,41 @@ struct ScaleOp {
   float s;
   int mode;
   struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
   __device__ bool active() const { return true; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
-  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
-    storeN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+    st<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
 };
 
 template <int N, int DT>
 struct SqnormOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 1;
   static constexpr int kKind = GS_OP_SQNORM;
   float* partials = nullptr;
   int slot;
   struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
   __device__ bool active() const { return true; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
-  __device__ void apply(const TV&, int64_t, Frag& f, float& acc) const {
+  template <bool F>
+  __device__ void apply(const TV&, int64_t, uint32_t, Frag& f, float& acc) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) acc = fmaf(f.x[i], f.x[i], acc);
   }
@@ -561,26 +862,32 @@ struct SqnormOp {
 template <int N, int DT>
 struct UnscaleOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 2;
   static constexpr int kKind = GS_OP_UNSCALE;
   float* partials = nullptr;
   int slot;
   const float* inv;  // nullable
   struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
   __device__ bool active() const { return true; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    loadN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
-  __device__ void apply(const TV& v, int64_t e, Frag& f, float& acc) const {
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float& acc) const {
 #pragma unroll
     for (int i = 0; i < N; ++i)
-      if (e + i < v.numel && !isfinite(f.x[i])) acc = 1.f;
+      if ((F || e0 + lo + i < v.numel) && !isfinite(f.x[i])) acc = 1.f;
     if (inv) {
       const float s = *inv;
       if (s != 1.f) {
 #pragma unroll
         for (int i = 0; i < N; ++i) f.x[i] = f.x[i] * s;
-        storeN<DT, N>(v.ptr[slot], e, v.numel, v.vec(slot), f.x);
+        st<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
       }
     }
   }
@@ -590,6 +897,7 @@ struct UnscaleOp {
 template <int N, int GD, int LD>
 struct SgdOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_SGD;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_SGD;
   float* partials = nullptr;
@@ -598,13 +906,19 @@ struct SgdOp {
   const float* found_inf;
   const float* hyper = nullptr;  // [lr] in device memory (gs_plan_set_hyper_source)
   struct Frag { float p[N], g[N], b[N]; };
+  __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
-  __device__ void load(const TV& v, int64_t e, Frag& f) const {
-    loadN<GS_F32, N>(v.ptr[0], e, v.numel, v.vec(0), f.p);
-    loadN<GD, N>(v.ptr[1], e, v.numel, v.vec(1), f.g);
-    if (h.mom != 0.f && !h.first) loadN<GS_F32, N>(v.ptr[2], e, v.numel, v.vec(2), f.b);
+  __device__ bool fast_ok(const TV& v) const {
+    return v.vec(0) && v.vec(1) && (h.mom == 0.f || v.vec(2)) && (LD < 0 || v.vec(3));
   }
-  __device__ void apply(const TV& v, int64_t e, Frag& f, float&) const {
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    ld<GD, N, F>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
+    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -621,9 +935,9 @@ struct SgdOp {
       }
       f.p[i] = fmaf(-h.lr, d, f.p[i]);              // param.add_(d, alpha=-lr)
     }
-    storeN<GS_F32, N>(v.ptr[0], e, v.numel, v.vec(0), f.p);
-    if (h.mom != 0.f) storeN<GS_F32, N>(v.ptr[2], e, v.numel, v.vec(2), f.b);
-    if constexpr (LD >= 0) storeN<LD, N>(v.ptr[3], e, v.numel, v.vec(3), f.p);
+    st<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    if (h.mom != 0.f) st<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+    if constexpr (LD >= 0) st<LD, N, F>(v.ptr[3], e0, lo, v.numel, v.vec(3), f.p);
   }
 };
 
@@ -631,6 +945,7 @@ struct SgdOp {
 template <int N, int GD, int LD>
 struct AdamOp {
   static constexpr int kN = N;
+  static constexpr int kG = GS_G_ADAM;
   static constexpr int kRed = 0;
   static constexpr int kKind = GS_OP_ADAM;
   float* partials = nullptr;
@@ -639,14 +954,20 @@ struct AdamOp {
   const float* found_inf;
   const float* hyper = nullptr;  // [step_size, bc2_sqrt, 1 - lr*wd] in device memory
   struct Frag { float p[N], g[N], m[N], v[N]; };
+  __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
-  __device__ void load(const TV& tv, int64_t e, Frag& f) const {
-    loadN<GS_F32, N>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
-    loadN<GD, N>(tv.ptr[1], e, tv.numel, tv.vec(1), f.g);
-    loadN<GS_F32, N>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
-    loadN<GS_F32, N>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
+  __device__ bool fast_ok(const TV& tv) const {
+    return tv.vec(0) && tv.vec(1) && tv.vec(2) && tv.vec(3) && (LD < 0 || tv.vec(4));
   }
-  __device__ void apply(const TV& tv, int64_t e, Frag& f, float&) const {
+  template <bool F>
+  __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    ld<GD, N, F>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
+    ld<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    ld<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+  }
+  template <bool F>
+  __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {
     const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -664,16 +985,19 @@ struct AdamOp {
       p = fmaf(h.step_size, m / denom, p);                  // addcdiv_(m, denom, -lr/bc1)
       f.p[i] = p; f.m[i] = m; f.v[i] = v;
     }
-    storeN<GS_F32, N>(tv.ptr[0], e, tv.numel, tv.vec(0), f.p);
-    storeN<GS_F32, N>(tv.ptr[2], e, tv.numel, tv.vec(2), f.m);
-    storeN<GS_F32, N>(tv.ptr[3], e, tv.numel, tv.vec(3), f.v);
-    if constexpr (LD >= 0) storeN<LD, N>(tv.ptr[4], e, tv.numel, tv.vec(4), f.p);
+    st<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    st<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    st<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+    if constexpr (LD >= 0) st<LD, N, F>(tv.ptr[4], e0, lo, tv.numel, tv.vec(4), f.p);
   }
 };
 
 template <int N, int GD, int LD>
 __device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD>& op) {
-  if (op.hyper) op.h.lr = op.hyper[0];
+  if (op.hyper) {
+    op.h.lr = op.hyper[0];
+    if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
+  }
 }
 template <int N, int GD, int LD>
 __device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD>& op) {
@@ -721,12 +1045,26 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
   if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
-  hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(p->grid), dim3(kBlock), 0, s, p->args(), op);
+  const bool chunk = use_chunk_engine(Op::kKind) && !p->chunks.empty();
+  int grid = p->grid;
+  if (chunk) {
+    const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
+    const bool red = Op::kRed != 0 && red_out;
+    const int cap = red ? std::min(p->grid_cap, red_grid_cap()) : p->grid_cap;
+    grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
+    PlanArgs a = p->args();
+    a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
+    a.red_out = Op::kRed != 0 ? red_out : nullptr;
+    a.red_acc = accumulate;
+    hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
+  } else {
+    hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
+  }
   HIP_RET(hipGetLastError());
   if constexpr (Op::kRed != 0) {
-    if (red_out) {
-      hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kBlock), 0, s,
-                         (const float*)p->d_partials, p->grid, red_out, accumulate);
+    if (red_out && !(chunk && GS_FUSED_RED)) {
+      hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s,
+                         (const float*)p->d_partials, grid, red_out, accumulate);
       HIP_RET(hipGetLastError());
     }
   }
@@ -779,11 +1117,13 @@ int hip_plan_upload_static(gs_plan* p) {
   const size_t sz_segs = sizeof(Seg) * p->segs.size();
   const size_t sz_tb = sizeof(int32_t) * p->task_begin.size();
   const size_t sz_n = sizeof(int64_t) * p->n;
+  const size_t sz_ch = sizeof(ChunkDesc) * p->chunks.size();
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  const size_t total = al(sz_segs) + al(sz_tb) + al(sz_n) * 2 + 256;
+  // segs | task_begin | numel | off | chunks | voff | ticket (layout of gs_plan::args)
+  const size_t total = al(sz_segs) + al(sz_tb) + al(sz_n) * 3 + al(sz_ch) + 256;
   HIP_RET(hipMalloc(&p->d_static, total));
   char* base = static_cast<char*>(p->d_static);
-  std::vector<char> h(total, 0);
+  std::vector<char> h(total, 0);  // the ticket starts at 0; every fused reduction re-arms it
   size_t o = 0;
   if (sz_segs) std::memcpy(h.data() + o, p->segs.data(), sz_segs);
   o += al(sz_segs);
@@ -792,6 +1132,10 @@ int hip_plan_upload_static(gs_plan* p) {
   if (sz_n) std::memcpy(h.data() + o, p->numel.data(), sz_n);
   o += al(sz_n);
   if (sz_n) std::memcpy(h.data() + o, p->off.data(), sz_n);
+  o += al(sz_n);
+  if (sz_ch) std::memcpy(h.data() + o, p->chunks.data(), sz_ch);
+  o += al(sz_ch);
+  if (sz_n) std::memcpy(h.data() + o, p->voff.data(), sz_n);
   HIP_RET(hipMemcpy(base, h.data(), total, hipMemcpyHostToDevice));
   const size_t tb = table_bytes(p) + 16;
   HIP_RET(hipMalloc(&p->d_table, tb));

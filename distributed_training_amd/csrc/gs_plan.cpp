@@ -33,12 +33,55 @@ gs::PlanArgs gs_plan::args() const {
   a.numel = reinterpret_cast<const int64_t*>(base + o);
   o += al(sizeof(int64_t) * n);
   a.off = reinterpret_cast<const int64_t*>(base + o);
+  o += al(sizeof(int64_t) * n);
+  a.chunks = reinterpret_cast<const ChunkDesc*>(base + o);
+  o += al(sizeof(ChunkDesc) * chunks.size());
+  a.voff = reinterpret_cast<const int64_t*>(base + o);
+  o += al(sizeof(int64_t) * n);
+  a.ticket = reinterpret_cast<uint32_t*>(base + o);
+  a.red_out = nullptr;
+  a.red_acc = 0;
+  a.per_wg = 0;
   a.ptrs = static_cast<void* const*>(d_table);
   a.align = reinterpret_cast<const uint32_t*>(static_cast<char*>(d_table) +
                                               sizeof(void*) * GS_PLAN_SLOTS * n);
   a.n = n;
   a.n_tasks = static_cast<int32_t>(task_begin.size()) - 1;
+  a.n_chunks = static_cast<int32_t>(chunks.size());
   return a;
+}
+
+// Chunk map of the chunk-map engine (gs_common.h): virtual offsets and one
+// descriptor per kChunkElems elements of the virtual space.
+static void build_chunk_map(gs_plan* p) {
+  const int n = p->n;
+  p->voff.assign(n, 0);
+  int64_t cur = 0;
+  for (int t = 0; t < n; ++t) {
+    const int64_t m = p->numel[t];
+    const int64_t a = m >= kGroupElems ? kGroupElems : (m >= kChunkElems ? kChunkElems : kUnit);
+    cur = (cur + a - 1) / a * a;
+    p->voff[t] = cur;
+    cur += m;
+  }
+  const int64_t n_chunks = (cur + kChunkElems - 1) / kChunkElems;
+  p->chunks.assign(static_cast<size_t>(n_chunks), ChunkDesc{-1, -1});
+  int t = 0;
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const int64_t lo = c * kChunkElems, hi = lo + kChunkElems;
+    // skip tensors that end at or before this chunk (and empty ones)
+    while (t < n && p->voff[t] + p->numel[t] <= lo) ++t;
+    if (t >= n || p->voff[t] >= hi) continue;  // gap: empty chunk
+    // span = tensor indices [t, t + span) whose ranges may intersect the chunk
+    // (empty tensors inside the run are harmless: a lane's search picks the
+    // LAST index with voff <= e, which is the non-empty one holding e)
+    int span = 0;
+    for (int u = t; u < n && p->voff[u] < hi; ++u) span = u - t + 1;
+    ChunkDesc& d = p->chunks[static_cast<size_t>(c)];
+    d.t0 = t;
+    const bool full = p->voff[t] <= lo && p->voff[t] + p->numel[t] >= hi;
+    d.code = full ? 0 : span;
+  }
 }
 
 // Task size (units) of a plan.  Every task is one workgroup's work; 256 CUs
@@ -179,6 +222,8 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
     return v > 0 ? static_cast<int>(std::min<long>(v, kGridLimit)) : kMaxGrid;
   }();
   p->grid = std::max(1, std::min(n_tasks, grid_cap));
+  build_chunk_map(p);
+  p->grid_cap = grid_cap;
   p->h_ptrs.assign(static_cast<size_t>(GS_PLAN_SLOTS) * n_tensors, nullptr);
   p->h_align.assign(n_tensors, 0u);
   if (device_kind == GS_DEV_HIP) {
@@ -324,8 +369,13 @@ int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double mo
   PLAN_OK(p);
   GS_CHECK_ARG(!nesterov || (momentum > 0 && dampening == 0),
                "Nesterov momentum requires a momentum and zero dampening");
+  GS_CHECK_ARG(first_step >= 0 || (first_step == -1 && p->hyper != nullptr),
+               "gs_sgd_step: first_step = -1 (device flag) needs a hyper source");
   SgdHyper h = make_sgd(lr, momentum, dampening, weight_decay, nesterov, maximize, first_step);
-  if (p->kind == GS_DEV_HOST && p->hyper) h.lr = p->hyper[0];
+  if (p->kind == GS_DEV_HOST && p->hyper) {
+    h.lr = p->hyper[0];
+    if (h.first < 0) h.first = p->hyper[1] != 0.f;
+  }
   if (p->kind == GS_DEV_HOST) return host_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
   return hip_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
 }

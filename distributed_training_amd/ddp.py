@@ -76,6 +76,62 @@ def compute_bucket_assignment_by_size(tensors, size_limits, order=None):
     return out
 
 
+def split_last_bucket(buckets, nbytes, cap):
+    """Cap the LAST bucket in gradient-ready order (the conv1 / layer1 end of
+    backward, whose pack -> collective -> unpack chain is exposed) at `cap`
+    bytes: its last-ready members up to `cap` form a new final bucket, the
+    rest stay a bucket of their own (torch's first_bucket_bytes_cap idea,
+    T:include/torch/csrc/distributed/c10d/reducer.hpp:30-31, applied to the
+    other end).  Bucket membership changes no element's sum."""
+    if not buckets:
+        return buckets
+    last = list(buckets[-1])
+    tail, size = [], 0
+    while last and (not tail or size + nbytes[last[-1]] <= cap):
+        i = last.pop()
+        tail.insert(0, i)
+        size += nbytes[i]
+    out = [list(b) for b in buckets[:-1]]
+    if last:
+        out.append(last)
+    out.append(tail)
+    return out
+
+
+def xgmi_bucket_caps(allreduce_time, world: int, sizes_mib=(1, 4, 16, 64), efficiency: float = 0.85) -> dict:
+    """Bucket caps for point-to-point xGMI from the live all-reduce curve.
+
+    Fits t(S) = alpha + S*f/B (f = 2(n-1)/n, B = bus bandwidth) to the measured
+    times of `sizes_mib` and picks
+      * bucket cap C: the smallest bucket whose all-reduce runs at `efficiency`
+        of B, i.e. S*f/B >= efficiency * t(S)  <=>  C = efficiency/(1-efficiency) * alpha*B/f,
+        clamped to [4, 256] MiB — fewer, larger collectives while each bucket
+        still overlaps the backward that follows it;
+      * last-bucket cap L: the bucket whose transfer costs one alpha
+        (L = alpha*B/f, clamped to [256 KiB, C]) — bounds the exposed tail to
+        ~2*alpha + the pack/unpack of L.
+    allreduce_time(nbytes) -> seconds (identical on every rank)."""
+    f = 2.0 * (world - 1) / world
+    pts = [(m * 1024 * 1024, allreduce_time(m * 1024 * 1024)) for m in sizes_mib]
+    # least-squares line t = alpha + S * beta
+    n = len(pts)
+    sx = sum(p[0] for p in pts)
+    sy = sum(p[1] for p in pts)
+    sxx = sum(p[0] * p[0] for p in pts)
+    sxy = sum(p[0] * p[1] for p in pts)
+    beta = (n * sxy - sx * sy) / max(1e-30, n * sxx - sx * sx)
+    alpha = max(0.0, (sy - beta * sx) / n)
+    if beta <= 0:  # degenerate curve: keep torch's caps
+        beta = pts[-1][1] / pts[-1][0]
+    bus = f / beta  # bytes/s
+    cap = efficiency / (1 - efficiency) * alpha * bus / f
+    cap = int(min(256 * 2**20, max(4 * 2**20, cap)))
+    last = int(min(cap, max(256 * 1024, alpha * bus / f)))
+    return {"points": [{"bytes": b, "ms": t * 1e3, "bus_GBps": b * f / t / 1e9} for b, t in pts],
+            "alpha_us": alpha * 1e6, "bus_GBps": bus / 1e9, "bucket_cap_bytes": cap, "last_bucket_cap_bytes": last,
+            "efficiency": efficiency}
+
+
 def _as_words(t: torch.Tensor):
     """A view of buffer `t` the multi-tensor kernels can move bit for bit:
     fp32 / bf16 / fp16 as they are; 4- and 8-byte integer or fp64 tensors as
@@ -189,7 +245,7 @@ class DistributedDataParallel(nn.Module):
                  check_reduction=False, gradient_as_bucket_view=False, static_graph=False,
                  delay_all_reduce_named_params=None, param_to_hook_all_reduce=None, mixed_precision=None,
                  device_mesh=None, skip_all_reduce_unused_params=False, *, bucket_dtype=None,
-                 collective: str = "auto"):
+                 collective: str = "auto", bucket_policy: str = "torch", last_bucket_cap_mb=None):
         super().__init__()
         if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
             raise NotImplementedError("delay_all_reduce_named_params is outside the gradient-sync path")
@@ -259,6 +315,21 @@ class DistributedDataParallel(nn.Module):
             self._verify_param_shape_across_processes()
             self._sync_module_states()
 
+        # bucket policy: "torch" = torch's caps (1 MiB first bucket, bucket_cap_mb);
+        # "xgmi" = caps from the live all-reduce curve of this group (xgmi_bucket_caps)
+        if bucket_policy not in ("torch", "xgmi"):
+            raise ValueError(f"bucket_policy must be 'torch' or 'xgmi', got {bucket_policy!r}")
+        self.bucket_policy = bucket_policy
+        self._last_bucket_cap = None if last_bucket_cap_mb is None else int(last_bucket_cap_mb * 1024 * 1024)
+        self._xgmi_calibration = None
+        if bucket_policy == "xgmi" and self.world_size > 1:
+            cal = xgmi_bucket_caps(self._calib_allreduce, self.world_size)
+            self._xgmi_calibration = cal
+            if bucket_cap_mb is None:
+                self.bucket_bytes_cap = cal["bucket_cap_bytes"]
+            if last_bucket_cap_mb is None:
+                self._last_bucket_cap = cal["last_bucket_cap_bytes"]
+
         if static_graph or not find_unused_parameters:
             limits = [sys.maxsize]
         elif self.bucket_bytes_cap_default:
@@ -276,6 +347,7 @@ class DistributedDataParallel(nn.Module):
         self._stream = None
         self._pending: dict[int, Any] = {}
         self._num_iterations = 0
+        self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
         self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                               for i, p in enumerate(self._params)]
 
@@ -299,6 +371,36 @@ class DistributedDataParallel(nn.Module):
         if t is not None:
             L.check(L.lib().gs_bucketer_set_found_inf(b.handle, t.data_ptr()), "gs_bucketer_set_found_inf")
         return b
+
+    def _calib_allreduce(self, nbytes: int, iters: int = 4) -> float:
+        """Median time (s, MAX over ranks) of one SUM all-reduce of nbytes of
+        fp32 through this DDP's collective (libgsync RCCL on its stream, or the
+        process group)."""
+        import time
+
+        n = max(1, nbytes // 4)
+        on_dev = self._comm is not None or self._backend == "nccl"
+        buf = torch.zeros(n, dtype=torch.float32, device=self.device if on_dev else "cpu")
+        ts = []
+        for it in range(iters + 1):
+            if on_dev:
+                torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.process_group)
+            t0 = time.perf_counter()
+            if self._comm is not None:
+                self._comm.all_reduce(buf, stream=L.stream_ptr(self.device))
+                torch.cuda.synchronize(self.device)
+            else:
+                dist.all_reduce(buf, group=self.process_group)
+                if on_dev:
+                    torch.cuda.synchronize(self.device)
+            if it:
+                ts.append(time.perf_counter() - t0)
+        ts.sort()
+        t = torch.tensor([ts[len(ts) // 2]], dtype=torch.float64,
+                         device=self.device if self._backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        return float(t.item())
 
     def _verify_param_shape_across_processes(self):
         if self.world_size == 1:
@@ -469,6 +571,9 @@ class DistributedDataParallel(nn.Module):
                 dense = torch.empty_like(param)
                 dense.copy_(g)
                 param.grad = g = dense
+            cap = self._capture_local
+            if cap is not None and idx in cap:
+                cap[idx] = g.detach().clone()  # on the producer stream, before the pack
             b = self._bucketer
             L.check(L.lib().gs_bucketer_mark_ready(b.handle, idx, g.data_ptr(), self._stream, b._ready,
                                                    ctypes.byref(b._n_ready)), "gs_bucketer_mark_ready")
@@ -530,6 +635,9 @@ class DistributedDataParallel(nn.Module):
             return
         limits = [self.first_bucket_bytes_cap, self.bucket_bytes_cap]
         buckets = compute_bucket_assignment_by_size(self._params, limits, order=self._ready_order)
+        if self._last_bucket_cap is not None:
+            buckets = split_last_bucket(buckets, [p.numel() * p.element_size() for p in self._params],
+                                        self._last_bucket_cap)
         buckets = self._sync_bucket_indices(buckets)
         if self.gradient_as_bucket_view:
             for p in self._params:  # grads must not alias the old buckets once they are freed
@@ -595,6 +703,31 @@ class DistributedDataParallel(nn.Module):
             out.append(ms.value)
         return out
 
+    def bucket_timeline_ms(self):
+        """Per-bucket timeline of the last iteration (gs_bucketer_last_timing):
+        list of dicts queue / pack / collective / unpack / ready_to_done, ms
+        (None where untimed: host buckets, external collectives, hipGraph replays)."""
+        out = []
+        buf = (ctypes.c_float * 5)()
+        for bi in range(len(self._bucketer.buckets)):
+            L.check(L.lib().gs_bucketer_last_timing(self._bucketer.handle, bi, buf), "gs_bucketer_last_timing")
+            v = [float(buf[k]) if buf[k] >= 0 else None for k in range(5)]
+            out.append(dict(zip(("queue", "pack", "collective", "unpack", "ready_to_done"), v)))
+        return out
+
+    def tail_ms(self):
+        """The exposed end-of-backward tail of the last iteration: from the
+        last bucket's ready event (its last gradient produced) to the
+        finalize event every bucket's chain has passed, split into the last
+        bucket's queue / pack / collective / unpack (HIP events)."""
+        tl = self.bucket_timeline_ms()
+        if not tl or tl[-1]["ready_to_done"] is None:
+            return None
+        last = tl[-1]
+        return {"total": last["ready_to_done"], "queue": last["queue"], "pack": last["pack"],
+                "collective": last["collective"], "unpack": last["unpack"],
+                "last_bucket_bytes": self._bucketer.buffers[-1].numel() * self._bucketer.buffers[-1].element_size()}
+
     def _get_ddp_logging_data(self):
         b = self._bucketer
         return {
@@ -611,6 +744,9 @@ class DistributedDataParallel(nn.Module):
             "rebuilt_bucket_sizes": b.logical_bytes() if self._has_rebuilt_buckets else [],
             "padded_bucket_numels": [buf.numel() for buf in b.buffers],
             "bucket_dtype": str(self._bucket_dtype),
+            "bucket_policy": self.bucket_policy,
+            "last_bucket_cap_bytes": self._last_bucket_cap,
+            "xgmi_calibration": self._xgmi_calibration,
             "num_parameter_tensors": len(self._params),
             "total_parameter_size_bytes": sum(p.numel() * p.element_size() for p in self._params),
         }

@@ -84,6 +84,9 @@ class TensorListPlan:
             raise ValueError(f"plan has {self.n} tensors, got {len(ptrs)} pointers")
         if self._slot_cache.get(slot) == ptrs:
             return
+        for t, n in zip(tensors_or_ptrs, self.numels):  # new pointers: the sizes must be the plan's
+            if isinstance(t, torch.Tensor) and t.numel() != n:
+                raise ValueError(f"plan tensor of {n} elements bound to a tensor of {t.numel()}")
         L.check(L.lib().gs_plan_set_ptrs(self.handle, slot, L.ptr_array(ptrs), None), "gs_plan_set_ptrs")
         self._slot_cache[slot] = ptrs
 
@@ -164,7 +167,7 @@ class TensorListPlan:
             L.lib().gs_sgd_step(
                 self.handle, L.gs_dtype(grad_dtype), -1 if lowp_dtype is None else L.gs_dtype(lowp_dtype),
                 float(lr), float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)),
-                int(bool(maximize)), int(bool(first_step)),
+                int(bool(maximize)), -1 if first_step == -1 else int(bool(first_step)),
                 None if grad_scale is None else grad_scale.data_ptr(),
                 None if found_inf is None else found_inf.data_ptr(), self._stream(stream)),
             "gs_sgd_step",

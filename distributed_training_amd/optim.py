@@ -45,10 +45,6 @@ def _capturing() -> bool:
     return torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()
 
 
-def _group_key(tensors):
-    return tuple((t.data_ptr(), t.numel()) for t in tensors)
-
-
 class _PlanCache:
     """One TensorListPlan per (param list, grad dtype) signature."""
 
@@ -136,13 +132,14 @@ class _FusedBase(torch.optim.Optimizer):
         return [ms for plan in self._plans.plans() if plan.kind == L.GS_DEV_HIP
                 for ms in plan.timer_read(kind=kind)]
 
-    def _skipped_on_host(self) -> bool:
-        """Host read of the AMP ``found_inf`` flag, for the cases a device-side
-        skip cannot express: torch skips ``optimizer.step()`` entirely on an
-        overflow (T:amp/grad_scaler.py ``_maybe_opt_step``), so a skipped step
-        must neither create momentum buffers (SGD's first step is buf = g) nor
-        advance Adam's step count (its bias corrections are host doubles)."""
-        return self.found_inf is not None and bool(self.found_inf.item() != 0)
+    def _device_state(self) -> bool:
+        """Step-varying state on the device: capturable mode, the AMP path
+        (``found_inf`` set: torch skips ``optimizer.step()`` entirely on an
+        overflow, T:amp/grad_scaler.py ``_maybe_opt_step`` — here the kernels
+        skip on the device and SGD's first-step flag / Adam's step counter
+        advance only on a clean step, so nothing is read on the host), or once
+        a group already keeps its counters there."""
+        return self.capturable or self.found_inf is not None or bool(self._dev_hyper)
 
     def _clip_scale(self, device, all_plans):
         """DeepSpeed-style gradient_clipping folded into the update: returns the
@@ -200,7 +197,7 @@ class FusedSGD(_FusedBase):
             buf = st.get("momentum_buffer")
             first = group["momentum"] != 0 and buf is None
             if group["momentum"] != 0 and buf is None:
-                buf = torch.empty_like(p, memory_format=torch.preserve_format)
+                buf = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["momentum_buffer"] = buf
             key = (p.grad.dtype, first)
             out.setdefault(key, ([], [], []))
@@ -220,8 +217,7 @@ class FusedSGD(_FusedBase):
                        for group in self.param_groups for p in group["params"])
         if new_bufs and _capturing():
             raise RuntimeError("FusedSGD: momentum buffers must exist before capture (take an eager step first)")
-        if new_bufs and self._skipped_on_host():
-            return loss
+        dev_state = self._device_state()
         work = []
         for gi, group in enumerate(self.param_groups):
             for (gdt, first), (ps, gs, bs) in self._collect(group).items():
@@ -229,19 +225,35 @@ class FusedSGD(_FusedBase):
                 plan.set_ptrs(0, ps)
                 plan.set_ptrs(1, gs)
                 plan.set_ptrs(2, [b.data_ptr() if b is not None else 0 for b in bs])
-                if self.capturable:
+                flag = None
+                if dev_state:
                     h = self._group_hyper(gi, group, ps[0].device)
                     if getattr(plan, "_hyper", None) is not h["hyper"]:
                         plan.set_hyper_source(h["hyper"])
-                work.append((group, plan, gdt, first))
-        if self.capturable:
+                    if group["momentum"] != 0:
+                        # first-step flag on the device (hyper[1]): set when this
+                        # step creates the buffers, cleared after a step that ran
+                        flag = h.setdefault("first_flags", {}).setdefault(
+                            id(plan), torch.zeros(1, dtype=torch.float32, device=ps[0].device))
+                        if first:
+                            flag.fill_(1.0)
+                work.append((group, plan, gdt, first, h if dev_state else None, flag))
+        if dev_state:
             self.refresh_hyper()
         if not work:
             return loss
         scale = self._clip_scale(work[0][1].device, [(w[1], w[2]) for w in work])
-        for group, plan, gdt, first in work:
+        for group, plan, gdt, first, h, flag in work:
+            if flag is not None:
+                h["hyper"][1:2].copy_(flag)
             plan.sgd(gdt, group["lr"], group["momentum"], group["dampening"], group["weight_decay"],
-                     group["nesterov"], group["maximize"], first, grad_scale=scale, found_inf=self.found_inf)
+                     group["nesterov"], group["maximize"], -1 if flag is not None else first,
+                     grad_scale=scale, found_inf=self.found_inf)
+            if flag is not None:
+                if self.found_inf is not None:
+                    flag.mul_(self.found_inf)  # kept only when the step was skipped
+                else:
+                    flag.zero_()
         return loss
 
 
@@ -273,9 +285,7 @@ class FusedAdam(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        cap = self.capturable
-        if not cap and self._skipped_on_host():
-            return loss
+        cap = self._device_state()  # device step counter: capturable or AMP (no host read of found_inf)
         work = []
         for gi, group in enumerate(self.param_groups):
             buckets = {}
@@ -395,7 +405,7 @@ def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm:
     sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
     plans = []
     for i, (dt, gl) in enumerate(groups.items()):
-        key = tuple(id(g) for g in gl) + (dev,)
+        key = tuple(g.numel() for g in gl) + (dev,)  # sizes + device: grad ids are reused after zero_grad
         plan = _NORM_PLANS.get(key)
         if plan is None:
             plan = TensorListPlan([g.numel() for g in gl], dev)

@@ -131,6 +131,7 @@ class ZeroDataParallel:
         self._queued = False
         self._pending = {}
         self._scratch = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
 
     # ------------------------------------------------------------------ setup
     def _bcast(self, t):
@@ -241,6 +242,9 @@ class ZeroDataParallel:
                 dense = torch.empty_like(param)
                 dense.copy_(g)
                 g = dense
+            cap = self._capture_local
+            if cap is not None and idx in cap:
+                cap[idx] = g.detach().clone()  # on the producer stream, before the pack
             # hold the grad until its bucket's pack is enqueued; param.grad is
             # released now (DeepSpeed frees it too)
             self._held.setdefault(self.loc[idx][0], []).append(g)

@@ -232,7 +232,9 @@ int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double b
                  const float* found_inf_dev, void* stream);
 /* Step-varying hyper-parameters from memory instead of the arguments: with a
  * non-NULL source, every later gs_sgd_step / gs_adam_step on this plan reads
- *   SGD:  hyper[0] = lr
+ *   SGD:  hyper[0] = lr; hyper[1] = "first step" flag (buf = g) when gs_sgd_step
+ *         is called with first_step = -1 — the AMP path keeps it on the device
+ *         (cleared by the caller after a step that was not skipped)
  *   Adam: hyper[0] = step_size (-lr/bc1), hyper[1] = bias_correction2_sqrt,
  *         hyper[2] = 1 - lr*wd (AdamW decay)
  * (fp32, device memory for HIP plans, host memory for host plans) when the
@@ -312,6 +314,13 @@ int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf);
 int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
 /* timing of the library's own collective launches (ms of the last iteration, via events) */
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
+/* per-bucket timeline of the last iteration (HIP events; -1 where untimed:
+ * host buckets, external collectives, hipGraph capture), ms:
+ *   out[0] queue      bucket ready on the producer -> comm stream starts it
+ *   out[1] pack       out[2] collective       out[3] unpack (+ fused checks)
+ *   out[4] ready -> every bucket finished (the finalize event): for the last
+ *          bucket this is the exposed end-of-backward tail */
+int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out /* [5] */);
 
 /* ====================================================================
  * Input step of the CIFAR configuration

@@ -75,6 +75,20 @@ def worker(rank, args, q):
     dist.destroy_process_group()
 
 
+def cpu_model_name() -> str:
+    """The host CPU model (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
 def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29777, ar_iters=3):
     if cores is None:
         cores = min(16, os.cpu_count() or 1)
@@ -100,6 +114,7 @@ def run(model="resnet50", batch=16, ws=2, cores=None, steps=3, warmup=1, port=29
         "batch_per_rank": batch,
         "steps": steps,
         "model": model,
+        "cpu_model": cpu_model_name(),
     }
 
 

@@ -44,15 +44,20 @@ def _reference(rank, ws, port, steps, batch, n, q):
     opt = torch.optim.Adam(model.parameters(), lr=1e-3 * ws)
     crit = nn.CrossEntropyLoss()
     loader.sampler.set_epoch(0)
+    grads = {}
     for k, (x, y) in enumerate(loader):
         if k >= steps:
             break
         loss = crit(model(x), y)
         loss.backward()
+        for name, p in model.module.named_parameters():  # the averaged grads Adam sees
+            grads[f"grad/{k}/{name}"] = p.grad.detach().numpy().copy()
         opt.step()
         opt.zero_grad()
     if rank == 0:
-        q.put({k: v.detach().numpy().copy() for k, v in model.module.state_dict().items()})
+        out = {k: v.detach().numpy().copy() for k, v in model.module.state_dict().items()}
+        out.update(grads)
+        q.put(out)
     dist.destroy_process_group()
 
 
@@ -83,7 +88,28 @@ def _run(fn, ws, steps, batch, n):
     return {k: torch.from_numpy(v) for k, v in out.items()}
 
 
+def _adam_close(ref, mine, steps, lr, eps=1e-8):
+    """SURVEY.md §8c Adam tolerance on the parameters: |Δ| <= steps·lr·1e-3,
+    excluding elements whose averaged grad had |ĝ| < 1e3·eps at some step (the
+    normalised update m/(√v+eps) can flip sign there).  Returns (worst, excluded
+    fraction)."""
+    worst, excl, total, over = 0.0, 0, 0, 0
+    tol = steps * lr * 1e-3
+    for name in [k[len("grad/0/"):] for k in ref if k.startswith("grad/0/")]:
+        keep = np.ones(ref[name].shape, dtype=bool)
+        for s in range(steps):
+            keep &= np.abs(ref[f"grad/{s}/{name}"].numpy()) >= 1e3 * eps
+        d = (ref[name].double() - mine[name].double()).abs().numpy()
+        if keep.any():
+            worst = max(worst, float(d[keep].max()))
+            over += int((d[keep] > tol).sum())
+        excl += int((~keep).sum())
+        total += keep.size
+    return worst, excl / total, over / total
+
+
 def _compare(ref, mine):
+    ref = {k: v for k, v in ref.items() if not k.startswith("grad/")}
     assert ref.keys() == mine.keys()
     fl = [k for k in ref if ref[k].is_floating_point()]
     for k in ref:
@@ -101,18 +127,30 @@ def _compare(ref, mine):
 def test_example_trainer_one_step_matches_reference():
     """One step: same batches, bit-identical averaged grads, Adam within last bits."""
     ws, batch, n = 2, 16, 400
-    worst, rel, frac = _compare(_run(_reference, ws, 1, batch, n), _run(_mine, ws, 1, batch, n))
+    ref, mine = _run(_reference, ws, 1, batch, n), _run(_mine, ws, 1, batch, n)
+    worst, rel, frac = _compare(ref, mine)
     assert worst <= 1e-7 and rel <= 1e-6, (worst, rel)
+    worst, _, over = _adam_close(ref, mine, 1, 1e-3 * ws)
+    assert over == 0, (worst, over)  # one step: every kept element within lr·1e-3
 
 
 def test_example_trainer_three_steps_track_reference():
-    """Three steps: Adam's normalised update amplifies last-bit differences where
-    |g| ~ eps, so the check is on the whole trajectory: relative
-    L2 distance <= 1e-4 of the distance travelled, <= 0.01 % of elements off by
-    > 1e-5 (observed: 1.7e-5 and 0.0014 %)."""
+    """Three steps.  After step 1 the weights differ in the last bits, so the
+    step-2/3 grads carry backprop round-off, which Adam's normalised update
+    m/(√v+eps) turns into a relative change for small |g| — an element-wise
+    one-step bound cannot hold along a trajectory.  Checked: of the elements
+    with |ĝ| >= 1e3·eps at every step (SURVEY.md §8c's exclusion; 37 % of
+    ResNet-18's elements at batch 16), <= 0.01 % beyond steps·lr·1e-3 and none
+    beyond 0.1·lr (observed: 0.003 % and 0.05·lr); the whole trajectory within
+    1e-4 relative L2 of the distance travelled.  The one-step test holds every
+    kept element to lr·1e-3."""
     ws, batch, n = 2, 16, 400
-    worst, rel, frac = _compare(_run(_reference, ws, 3, batch, n), _run(_mine, ws, 3, batch, n))
-    assert rel <= 1e-4 and frac <= 1e-4 and worst <= 3 * 2 * 2e-3, (worst, rel, frac)
+    ref, mine = _run(_reference, ws, 3, batch, n), _run(_mine, ws, 3, batch, n)
+    worst, rel, frac = _compare(ref, mine)
+    assert rel <= 1e-4 and frac <= 1e-4, (worst, rel, frac)
+    lr = 1e-3 * ws
+    worst, excluded, over = _adam_close(ref, mine, 3, lr)  # SURVEY §8c off the |g|<1e-5 set
+    assert over <= 1e-4 and worst <= 0.1 * lr, (worst, excluded, over)
 
 
 def _init():

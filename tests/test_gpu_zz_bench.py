@@ -63,6 +63,11 @@ def _check_line(d, n):
     g = d["grad_sync"]
     assert g["n_buckets"] == len(g["bucket_bytes"]) >= 1
     assert g["grad_bytes_per_step"] == 4 * d["config"]["params"]
+    # the self-check step after the timed region (distributed_training_amd/parity.py)
+    p = d["parity"]
+    assert p is not None and p["ok"] is True and p["world"] == n, p
+    assert p["averaged_grads"]["bitwise_equal"] is True and p["weights_identical"] is True
+    assert p["buffers_identical"] is True
 
 
 def test_bench_n1_contract(cuda_device):
@@ -73,6 +78,10 @@ def test_bench_n1_contract(cuda_device):
     assert len(lines) == 1, p.stdout[-2000:]
     _check_line(lines[0], 1)
     assert lines[0]["config"]["impl"] == "libgsync"
+    assert lines[0]["parity"]["collective"] == "rccl(libgsync)"
+    t = lines[0]["grad_sync"]["tail_ms"]  # last bucket ready -> every bucket chain done
+    assert t["total"] > 0 and t["pack"] > 0 and t["collective"] >= 0 and t["unpack"] > 0
+    assert len(lines[0]["grad_sync"]["bucket_timeline_ms"]) == lines[0]["grad_sync"]["n_buckets"]
 
 
 def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
@@ -86,3 +95,4 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
     _check_line(lines[0], 2)
     assert "rehearsal" in lines[0]["config"]
+    assert lines[0]["parity"]["collective"] == "gloo"
