@@ -37,7 +37,7 @@ GS_BKT_NO_SCALE = 4
 GS_BKT_REDUCE_SCATTER = 8
 GS_BKT_NO_UNPACK = 16
 GS_LAYOUT_NCHW, GS_LAYOUT_NHWC = 0, 1
-GS_OP_PACK, GS_OP_UNPACK, GS_OP_SCALE, GS_OP_SQNORM, GS_OP_UNSCALE, GS_OP_SGD, GS_OP_ADAM = 1, 2, 3, 4, 5, 6, 7
+GS_OP_PACK, GS_OP_UNPACK, GS_OP_SCALE, GS_OP_SQNORM, GS_OP_UNSCALE, GS_OP_SGD, GS_OP_ADAM, GS_OP_SUM = 1, 2, 3, 4, 5, 6, 7, 8
 
 _TORCH_TO_GS = {
     torch.float32: GS_F32,
@@ -95,6 +95,7 @@ SIGNATURES = {
     "gs_unpack_check": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "gs_scale": (_c_int, [_vp, _c_int, _c_int, _c_f, _c_int, _vp]),
     "gs_sqnorm": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
+    "gs_sum": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_rng_state_bytes": (_c_int, []),
     "gs_rng_draw_u32": (_c_int, [_vp, _c_i64, _c_i64, _vp]),
     "gs_randperm": (_c_int, [ctypes.c_uint64, _c_i64, _vp]),
@@ -134,6 +135,8 @@ SIGNATURES = {
     "gs_bucketer_finalize": (_c_int, [_vp, _vp]),
     "gs_bucketer_unpack_bucket": (_c_int, [_vp, _c_int, _vp]),
     "gs_bucketer_set_found_inf": (_c_int, [_vp, _vp]),
+    "gs_bucketer_set_debug": (_c_int, [_vp, _vp]),
+    "gs_bucketer_set_bucket_dtype": (_c_int, [_vp, _c_int, _c_int, _c_int]),
     "gs_bucketer_last_comm_ms": (_c_int, [_vp, _c_int, _p_f]),
     "gs_bucketer_last_timing": (_c_int, [_vp, _c_int, _p_f]),
 }

@@ -112,14 +112,18 @@ class WarmupLR:
         self.max_lr = warmup_max_lr
         self.warmup_num_steps = max(2, warmup_num_steps)
         self.warmup_type = warmup_type
-        # last_batch_iteration = index of the last completed optimizer step; the
-        # lr in the param groups is the one the NEXT step uses: warmup(last + 1)
+        # DeepSpeed's published schedule: construction leaves warmup_min_lr in the
+        # optimizer; step() (after each optimizer step) sets last_batch_iteration
+        # += 1 and lr = min + (max - min) * gamma(last_batch_iteration) with
+        # gamma(i) = log(i + 1) / log(N) — lrs of steps 1, 2, 3: min, min, gamma(1)
         self.last_batch_iteration = last_batch_iteration
-        self._set(self.get_lr()[0])
+        self._set(self.min_lr if last_batch_iteration < 0 else self.get_lr()[0])
 
     def get_lr(self):
-        it = max(0, self.last_batch_iteration + 1)
-        return [warmup_lr(it, self.min_lr, self.max_lr, self.warmup_num_steps, self.warmup_type)]
+        if self.last_batch_iteration < 0:  # DeepSpeed warns "before it has started" and returns [0.0]
+            return [0.0]
+        return [warmup_lr(self.last_batch_iteration, self.min_lr, self.max_lr, self.warmup_num_steps,
+                          self.warmup_type)]
 
     def get_last_lr(self):
         return [g["lr"] for g in self.optimizer.param_groups]
@@ -137,7 +141,7 @@ class WarmupLR:
 
     def load_state_dict(self, sd):
         self.last_batch_iteration = sd["last_batch_iteration"]
-        self._set(self.get_lr()[0])
+        self._set(self.min_lr if self.last_batch_iteration < 0 else self.get_lr()[0])
 
 
 class DeepSpeedEngine(nn.Module):

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <mutex>
 
 #include "gs_common.h"
@@ -27,8 +28,7 @@ namespace gs {
 ncclComm_t comm_handle(gs_comm* c);
 hipStream_t comm_stream(gs_comm* c);
 int comm_dtype(int dt, ncclDataType_t* out);
-int comm_check_live(gs_comm* c);
-int comm_track(gs_comm* c, hipStream_t stream);
+int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what);
 }  // namespace gs
 
 using namespace gs;
@@ -47,6 +47,7 @@ struct Bucket {
   gs_plan* plan = nullptr;      // layout of the params inside the flat bucket
   gs_plan* flat = nullptr;      // the whole flat bucket as one tensor (in-place ops)
   int64_t numel = 0;            // padded flat numel
+  int gdt = GS_F32, bdt = GS_F32;  // grad / bucket dtype of this bucket (torch buckets per dtype)
   void* buf = nullptr;          // torch-owned flat storage
   void* shard = nullptr;        // torch-owned reduce-scatter output
   int pending = 0;
@@ -79,6 +80,7 @@ struct gs_bucketer {
   float* sqnorm = nullptr;
   int sq_count = 0;
   float* found_inf = nullptr;  // AMP non-finite flag of the averaged grads (fused into unpack)
+  float* dbg = nullptr;        // GSYNC_DEBUG: [3 * n_buckets] Σx after pack, Σx after collective, Σx² after pack
   void* producer = nullptr;
   hipEvent_t ev_done = nullptr;
   bool done_timed = false;
@@ -103,66 +105,82 @@ void plan_set_one(gs_plan* p, int slot, int t, void* ptr) {
   p->dirty = true;
 }
 
+int bucket_index(gs_bucketer* b, const Bucket& bk) { return static_cast<int>(&bk - b->buckets.data()); }
+
+// GSYNC_DEBUG checksums: Σ bucket after the pack (which = 0, before the
+// collective) / after the collective (which = 1, before the unpack)
+int debug_sum(gs_bucketer* b, Bucket& bk, int which, void* stream) {
+  if (!b->dbg) return GS_OK;
+  float* d = b->dbg + 3 * bucket_index(b, bk);
+  GS_TRY_RET(gs_sum(bk.flat, 0, bk.bdt, d + which, 0, stream));
+  // the packed bucket's Σx² sets the scale of the cross-rank comparison
+  return which == 0 ? gs_sqnorm(bk.flat, 0, bk.bdt, d + 2, 0, stream) : GS_OK;
+}
+
 // after the collective: unpack into the grads (with the fused Σg² or the fused
 // non-finite check), or, when the grads ARE the bucket, just the check
 int unpack_one(gs_bucketer* b, Bucket& bk, void* stream, int accumulate_sq) {
   float* sq = b->sqnorm;
   if (b->do_unpack()) {
     if (b->found_inf && !sq) {
-      GS_TRY_RET(gs_unpack_check(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, b->found_inf, stream));
+      GS_TRY_RET(gs_unpack_check(bk.plan, bk.buf, bk.bdt, 1, bk.gdt, b->found_inf, stream));
     } else {
       const int acc = (b->sq_count > 0 || accumulate_sq) ? 1 : 0;
-      GS_TRY_RET(gs_unpack(bk.plan, bk.buf, b->bucket_dtype, 1, b->grad_dtype, sq, acc, stream));
+      GS_TRY_RET(gs_unpack(bk.plan, bk.buf, bk.bdt, 1, bk.gdt, sq, acc, stream));
       if (sq) ++b->sq_count;
-      if (b->found_inf) GS_TRY_RET(gs_unscale_check(bk.flat, 0, b->bucket_dtype, nullptr, b->found_inf, stream));
+      if (b->found_inf) GS_TRY_RET(gs_unscale_check(bk.flat, 0, bk.bdt, nullptr, b->found_inf, stream));
     }
   } else if (b->found_inf) {
-    GS_TRY_RET(gs_unscale_check(bk.flat, 0, b->bucket_dtype, nullptr, b->found_inf, stream));
+    GS_TRY_RET(gs_unscale_check(bk.flat, 0, bk.bdt, nullptr, b->found_inf, stream));
   }
   bk.unpacked = true;
   return GS_OK;
 }
 
 // pack (or scale in place) bucket bk on `stream`
-int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
+int pack_raw(gs_bucketer* b, Bucket& bk, void* stream) {
   const bool no_scale = (b->flags & GS_BKT_NO_SCALE) != 0;
   if (b->flags & GS_BKT_GRAD_VIEW) {
     // grads alias the bucket (gradient_as_bucket_view): bucket_view.div_(div_factor)
     bool all_alias = true;
-    const int es = dtype_size(b->bucket_dtype);
+    const int es = dtype_size(bk.bdt);
     for (size_t i = 0; i < bk.params.size(); ++i) {
       const void* g = bk.plan->h_ptrs[static_cast<size_t>(1) * bk.plan->n + i];
       if (g != static_cast<char*>(bk.buf) + bk.plan->off[i] * es) { all_alias = false; break; }
     }
     if (all_alias) {
       if (no_scale || b->div == 1.f) return GS_OK;
-      return gs_scale(bk.flat, 0, b->bucket_dtype, b->div, GS_SCALE_DIV, stream);
+      return gs_scale(bk.flat, 0, bk.bdt, b->div, GS_SCALE_DIV, stream);
     }
   }
-  if (no_scale) return gs_pack(bk.plan, 1, b->grad_dtype, bk.buf, b->bucket_dtype, 1.f, GS_SCALE_NONE, stream);
+  if (no_scale) return gs_pack(bk.plan, 1, bk.gdt, bk.buf, bk.bdt, 1.f, GS_SCALE_NONE, stream);
   // at::mul_out(bucket_view, grad, 1/div_factor): the scalar is float(1.0/div)
   const float inv = static_cast<float>(1.0 / static_cast<double>(b->div));
-  return gs_pack(bk.plan, 1, b->grad_dtype, bk.buf, b->bucket_dtype, inv, GS_SCALE_MUL, stream);
+  return gs_pack(bk.plan, 1, bk.gdt, bk.buf, bk.bdt, inv, GS_SCALE_MUL, stream);
+}
+
+int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
+  GS_TRY_RET(pack_raw(b, bk, stream));
+  return debug_sum(b, bk, 0, stream);
 }
 
 int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
-  GS_TRY_RET(comm_check_live(b->comm));
   ncclDataType_t dt;
-  GS_TRY_RET(comm_dtype(b->bucket_dtype, &dt));
-  ncclResult_t r;
+  GS_TRY_RET(comm_dtype(bk.bdt, &dt));
   if (b->flags & GS_BKT_REDUCE_SCATTER) {
     const int w = gs_comm_world(b->comm);
-    r = ncclReduceScatter(bk.buf, bk.shard, static_cast<size_t>(bk.numel / w), dt, ncclSum,
-                          comm_handle(b->comm), cs);
-  } else {
-    r = ncclAllReduce(bk.buf, bk.buf, static_cast<size_t>(bk.numel), dt, ncclSum,
-                      comm_handle(b->comm), cs);
+    return comm_enqueue(b->comm, cs, [&] {
+      return ncclReduceScatter(bk.buf, bk.shard, static_cast<size_t>(bk.numel / w), dt, ncclSum,
+                               comm_handle(b->comm), cs);
+    }, "bucket reduce-scatter");
   }
-  if (r != ncclSuccess) return fail(GS_ERCCL, std::string("bucket collective: ") + ncclGetErrorString(r));
-  return comm_track(b->comm, cs);
+  return comm_enqueue(b->comm, cs, [&] {
+    return ncclAllReduce(bk.buf, bk.buf, static_cast<size_t>(bk.numel), dt, ncclSum, comm_handle(b->comm), cs);
+  }, "bucket all-reduce");
 }
 
 int launch_bucket(gs_bucketer* b, int bi) {
+  GsRange range("gsync.bucket");
   Bucket& bk = b->buckets[bi];
   if (!bk.buf) return fail(GS_ESTATE, "bucket " + std::to_string(bi) + " has no storage");
   if (!b->hip()) {
@@ -179,6 +197,7 @@ int launch_bucket(gs_bucketer* b, int bi) {
     GS_TRY_RET(launch_collective(b, bk, cs));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
     bk.timed = timed;
+    GS_TRY_RET(debug_sum(b, bk, 1, cs));
     if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_u1, cs));
   } else {
@@ -265,6 +284,8 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     rc = gs_plan_create(device_kind, device, 1, &bk.numel, 0, &bk.flat);
     if (rc != GS_OK) return bail(rc);
     bk.pending = static_cast<int>(bk.params.size());
+    bk.gdt = grad_dtype;
+    bk.bdt = bucket_dtype;
     if (device_kind == GS_DEV_HIP) {
       if (hipEventCreate(&bk.ev_ready) != hipSuccess || hipEventCreate(&bk.ev_pk0) != hipSuccess ||
           hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess ||
@@ -313,6 +334,17 @@ int gs_bucketer_param_location(gs_bucketer* b, int param, int32_t* bucket, int64
   const int bi = b->loc_bucket[param];
   if (bucket) *bucket = bi;
   if (offset) *offset = b->buckets[bi].plan->off[b->loc_intra[param]];
+  return GS_OK;
+}
+
+int gs_bucketer_set_bucket_dtype(gs_bucketer* b, int bucket, int grad_dtype, int bucket_dtype) {
+  GS_CHECK_ARG(b && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
+  GS_CHECK_ARG(is_float_dtype(grad_dtype) && is_float_dtype(bucket_dtype),
+               "gs_bucketer_set_bucket_dtype: grad and bucket dtypes must be floating");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->prepared) return fail(GS_ESTATE, "gs_bucketer_set_bucket_dtype inside a backward");
+  b->buckets[bucket].gdt = grad_dtype;
+  b->buckets[bucket].bdt = bucket_dtype;
   return GS_OK;
 }
 
@@ -385,6 +417,7 @@ int gs_bucketer_mark_unused(gs_bucketer* b, void* stream, int32_t* ready_out, in
 
 int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
   GS_CHECK_ARG(b != nullptr, "gs_bucketer_finalize: NULL bucketer");
+  GsRange range("gsync.finalize");
   std::lock_guard<std::mutex> lk(b->mu);
   if (!b->prepared) return fail(GS_ESTATE, "finalize without prepare");
   if (b->next_bucket != static_cast<int>(b->buckets.size())) {
@@ -401,9 +434,13 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
     HIPB_RET(hipEventRecord(b->ev_done, cs));
     b->done_timed = !stream_capturing(cs);
     HIPB_RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), b->ev_done, 0));
-  } else if (b->do_unpack() || b->found_inf) {
-    for (Bucket& bk : b->buckets)
-      if (!bk.unpacked) GS_TRY_RET(unpack_one(b, bk, stream, 0));
+  } else {
+    // external collectives (comm hook / process group) are done by now
+    for (Bucket& bk : b->buckets) {
+      if (bk.unpacked) continue;
+      GS_TRY_RET(debug_sum(b, bk, 1, stream));
+      if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, stream, 0));
+    }
   }
   b->prepared = false;
   return GS_OK;
@@ -415,6 +452,15 @@ int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf) {
                "gs_bucketer_set_found_inf: sharded (ZeRO) buckets check their shard in the optimizer");
   std::lock_guard<std::mutex> lk(b->mu);
   b->found_inf = found_inf;
+  return GS_OK;
+}
+
+int gs_bucketer_set_debug(gs_bucketer* b, float* sums) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_set_debug: NULL bucketer");
+  GS_CHECK_ARG(!(b->flags & GS_BKT_REDUCE_SCATTER) || sums == nullptr,
+               "gs_bucketer_set_debug: reduce-scatter buckets keep only a shard after the collective");
+  std::lock_guard<std::mutex> lk(b->mu);
+  b->dbg = sums;
   return GS_OK;
 }
 

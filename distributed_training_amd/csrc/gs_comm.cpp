@@ -21,6 +21,7 @@
 #include <atomic>
 #include <chrono>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 
@@ -32,7 +33,7 @@ struct gs_comm {
   int rank = 0, world = 1, device = 0;
   std::atomic<bool> aborted{false};
   std::string abort_reason;
-  std::mutex mu;  // enqueue vs abort vs the watchdog's bookkeeping
+  std::mutex mu;  // enqueue (comm_enqueue) vs abort vs the watchdog's bookkeeping
   // watchdog
   int64_t timeout_ms = 0;
   std::thread wd;
@@ -108,10 +109,24 @@ std::atomic<int> g_wd_pause{0};
 void watchdog_loop(gs_comm* c) {
   (void)hipSetDevice(c->device);
   using clk = std::chrono::steady_clock;
+  auto busy_since = clk::time_point();
   while (!c->wd_stop.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
     if (g_wd_pause.load() > 0) continue;
-    std::lock_guard<std::mutex> lk(c->mu);
+    // enqueues hold c->mu for the few microseconds of an RCCL enqueue, so the
+    // abort never frees the communicator under a concurrent enqueue; only an
+    // enqueue that itself hangs (holding the lock past the timeout) is
+    // aborted without it — that enqueue is what the abort has to break
+    std::unique_lock<std::mutex> lk(c->mu, std::try_to_lock);
+    if (!lk.owns_lock()) {
+      if (busy_since == clk::time_point()) busy_since = clk::now();
+      const auto held = std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - busy_since);
+      if (c->timeout_ms > 0 && held.count() > c->timeout_ms && !c->aborted.load())
+        abort_locked(c, "watchdog: an RCCL enqueue has been blocked for " + std::to_string(held.count()) +
+                            " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
+      continue;
+    }
+    busy_since = clk::time_point();
     if (c->aborted.load()) continue;
     ncclResult_t async = ncclSuccess;
     if (c->comm && ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
@@ -139,18 +154,11 @@ ncclComm_t comm_handle(gs_comm* c) { return c->comm; }
 hipStream_t comm_stream(gs_comm* c) { return c->stream; }
 int comm_dtype(int dt, ncclDataType_t* out) { return to_nccl_dtype(dt, out); }
 
-// before enqueueing a collective: fails once the communicator is aborted
-int comm_check_live(gs_comm* c) {
-  if (!c) return fail(GS_EINVAL, "no communicator");
-  if (c->aborted.load()) return fail(GS_ERCCL, "communicator aborted: " + c->abort_reason);
-  return GS_OK;
-}
-
-// after enqueueing a collective on `stream`: hand its completion to the watchdog
-int comm_track(gs_comm* c, hipStream_t stream) {
+// caller holds c->mu: hand the completion of the collective just enqueued on
+// `stream` to the watchdog
+int comm_track_locked(gs_comm* c, hipStream_t stream) {
   // a collective recorded into a hipGraph runs at replay, not now: not tracked
   if (c->timeout_ms <= 0 || stream_capturing(stream)) return GS_OK;
-  std::lock_guard<std::mutex> lk(c->mu);
   hipEvent_t ev;
   if (!c->ev_pool.empty()) {
     ev = c->ev_pool.back();
@@ -164,6 +172,18 @@ int comm_track(gs_comm* c, hipStream_t stream) {
   }
   c->inflight.push_back({ev, std::chrono::steady_clock::now()});
   return GS_OK;
+}
+
+// Enqueue one RCCL collective under c->mu: liveness check, enqueue and
+// watchdog tracking are atomic with respect to the watchdog's abort.
+int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what) {
+  if (!c) return fail(GS_EINVAL, "no communicator");
+  GsRange range(what);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->aborted.load()) return fail(GS_ERCCL, "communicator aborted: " + c->abort_reason);
+  const ncclResult_t r = fn();
+  if (r != ncclSuccess) return rccl_fail(r, what);
+  return comm_track_locked(c, stream);
 }
 
 }  // namespace gs
@@ -282,47 +302,48 @@ int gs_comm_stream(gs_comm* c, void** stream_out) {
 int gs_allreduce(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
                  void* stream) {
   GS_CHECK_ARG(c != nullptr, "gs_allreduce: NULL communicator");
-  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   ncclRedOp_t o;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   GS_TRY_RET(to_nccl_op(op, &o));
-  RCCL_RET(ncclAllReduce(send, recv, static_cast<size_t>(count), dt, o, c->comm, pick(c, stream)));
-  return comm_track(c, pick(c, stream));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(c, s, [&] { return ncclAllReduce(send, recv, static_cast<size_t>(count), dt, o, c->comm, s); },
+                      "ncclAllReduce");
 }
 
 int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,
                       int op, void* stream) {
   GS_CHECK_ARG(c != nullptr, "gs_reduce_scatter: NULL communicator");
-  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   ncclRedOp_t o;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   GS_TRY_RET(to_nccl_op(op, &o));
-  RCCL_RET(ncclReduceScatter(send, recv, static_cast<size_t>(recv_count), dt, o, c->comm,
-                             pick(c, stream)));
-  return comm_track(c, pick(c, stream));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(
+      c, s, [&] { return ncclReduceScatter(send, recv, static_cast<size_t>(recv_count), dt, o, c->comm, s); },
+      "ncclReduceScatter");
 }
 
 int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
                   void* stream) {
   GS_CHECK_ARG(c != nullptr, "gs_all_gather: NULL communicator");
-  GS_TRY_RET(comm_check_live(c));
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
-  RCCL_RET(ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, pick(c, stream)));
-  return comm_track(c, pick(c, stream));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(c, s, [&] { return ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, s); },
+                      "ncclAllGather");
 }
 
 int gs_broadcast(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
                  void* stream) {
   GS_CHECK_ARG(c != nullptr, "gs_broadcast: NULL communicator");
-  GS_TRY_RET(comm_check_live(c));
   GS_CHECK_ARG(root >= 0 && root < c->world, "gs_broadcast: bad root");
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
-  RCCL_RET(ncclBroadcast(send, recv, static_cast<size_t>(count), dt, root, c->comm, pick(c, stream)));
-  return comm_track(c, pick(c, stream));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(
+      c, s, [&] { return ncclBroadcast(send, recv, static_cast<size_t>(count), dt, root, c->comm, s); },
+      "ncclBroadcast");
 }
 
 }  // extern "C"

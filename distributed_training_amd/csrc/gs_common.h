@@ -11,6 +11,24 @@
 
 namespace gs {
 
+// ---- roctx ranges (SURVEY.md §5 tracing): host-side ranges around every
+// pack / collective / unpack / update enqueue, visible in
+// `rocprofv3 --marker-trace`; off unless GSYNC_ROCTX=1 (one cached getenv)
+bool roctx_enabled();
+void roctx_push(const char* name);
+void roctx_pop();
+struct GsRange {
+  bool on;
+  explicit GsRange(const char* name) : on(roctx_enabled()) {
+    if (on) roctx_push(name);
+  }
+  ~GsRange() {
+    if (on) roctx_pop();
+  }
+  GsRange(const GsRange&) = delete;
+  GsRange& operator=(const GsRange&) = delete;
+};
+
 // ---- error plumbing: thread-local message, int codes across the ABI ----
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
@@ -237,6 +255,7 @@ int hip_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, in
                      void* stream);
 int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream);
 int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream);
+int hip_sum(gs_plan* p, int slot, int dt, float* out, int acc, void* stream);
 int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm,
                   void* stream);
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
@@ -256,6 +275,7 @@ int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst
 int host_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found);
 int host_scale(gs_plan* p, int slot, int dt, float s, int mode);
 int host_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc);
+int host_sum(gs_plan* p, int slot, int dt, float* out, int acc);
 int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm);
 int host_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found);
 int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi);

@@ -216,6 +216,18 @@ int host_sqnorm(gs_plan* p, int s_, int dt, float* sq, int acc) {
   return GS_OK;
 }
 
+int host_sum(gs_plan* p, int s_, int dt, float* out, int acc) {
+  GS_HOST_FLOAT(dt, DT, {
+    double total = 0.0;
+    for (int t = 0; t < p->n; ++t) {
+      const void* x = slot(p, s_, t);
+      for (int64_t i = 0; i < p->numel[t]; ++i) total += ldT<DT>(x, i);
+    }
+    out[0] = acc ? out[0] + static_cast<float>(total) : static_cast<float>(total);
+  });
+  return GS_OK;
+}
+
 int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm) {
   const float nrm = std::sqrt(sq[0]);
   if (norm) norm[0] = nrm;

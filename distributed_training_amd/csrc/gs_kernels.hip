@@ -683,22 +683,20 @@ bool use_chunk_engine(int kind) {
   }();
   return (mask >> kind) & 1;
 }
-// reductions: at most this many workgroups (= partials for the combine),
-// each taking a contiguous range of groups (GS_RED_CONTIG=1) or grid-striding;
-// GS_RED_GRID / GS_RED_CONTIG in the environment override (sweeps)
-#ifndef GS_RED_GRID
-#define GS_RED_GRID 2048
-#endif
+// reductions: at most Op::kRedGrid workgroups (= partials for the combine:
+// 8 Ki for the read-only Σg² / inf checks, uncapped for the unpack that
+// carries a fused Σg²; profiles/r2e_red.jsonl), each grid-striding or taking a
+// contiguous range of groups (GS_RED_CONTIG=1); GS_RED_GRID / GS_RED_CONTIG
+// in the environment override (sweeps)
 #ifndef GS_RED_CONTIG
 #define GS_RED_CONTIG 0
 #endif
-int red_grid_cap() {
+int red_grid_cap(int op_default) {
   static const int v = [] {
     const char* e = std::getenv("GS_RED_GRID");
-    const int x = e ? std::atoi(e) : GS_RED_GRID;
-    return std::max(1, std::min(x, kGridLimit));
+    return e ? std::max(1, std::min(std::atoi(e), kGridLimit)) : 0;
   }();
-  return v;
+  return v > 0 ? v : op_default;
 }
 bool red_contiguous() {
   static const bool v = [] {
@@ -728,6 +726,7 @@ struct PackOp {
   static constexpr int kN = N;
   static constexpr int kG = FD == GS_F32 ? GS_G_PACK : GS_G_PACK16;
   static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_PACK;
   float* partials = nullptr;
   int slot;
@@ -774,6 +773,7 @@ struct UnpackOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = RED;
+  static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
   bool want_red;
@@ -813,6 +813,7 @@ struct ScaleOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_SCALE;
   float* partials = nullptr;
   int slot;
@@ -840,6 +841,7 @@ struct SqnormOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 1;
+  static constexpr int kRedGrid = 8192;
   static constexpr int kKind = GS_OP_SQNORM;
   float* partials = nullptr;
   int slot;
@@ -859,11 +861,37 @@ struct SqnormOp {
   }
 };
 
+// Σ x (debug bucket checksums)
+template <int N, int DT>
+struct SumOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
+  static constexpr int kRed = 1;
+  static constexpr int kRedGrid = 8192;
+  static constexpr int kKind = GS_OP_SUM;
+  float* partials = nullptr;
+  int slot;
+  struct Frag { float x[N]; };
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV&, int64_t, uint32_t, Frag& f, float& acc) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc += f.x[i];
+  }
+};
+
 template <int N, int DT>
 struct UnscaleOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 2;
+  static constexpr int kRedGrid = 8192;
   static constexpr int kKind = GS_OP_UNSCALE;
   float* partials = nullptr;
   int slot;
@@ -899,6 +927,7 @@ struct SgdOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_SGD;
   static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_SGD;
   float* partials = nullptr;
   SgdHyper h;
@@ -947,6 +976,7 @@ struct AdamOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_ADAM;
   static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_ADAM;
   float* partials = nullptr;
   AdamHyper h;
@@ -1050,7 +1080,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   if (chunk) {
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
     const bool red = Op::kRed != 0 && red_out;
-    const int cap = red ? std::min(p->grid_cap, red_grid_cap()) : p->grid_cap;
+    const int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     PlanArgs a = p->args();
     a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
@@ -1361,6 +1391,16 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
     SqnormOp<GS_PACK_N, DT> op;
     op.slot = slot;
     return launch<GS_RED_ILP>(p, op, stream, sq, acc);
+  });
+  return GS_OK;
+}
+
+int hip_sum(gs_plan* p, int slot, int dt, float* out, int acc, void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(dt, DT, {
+    SumOp<GS_PACK_N, DT> op;
+    op.slot = slot;
+    return launch<GS_RED_ILP>(p, op, stream, out, acc);
   });
   return GS_OK;
 }

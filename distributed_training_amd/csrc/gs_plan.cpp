@@ -5,11 +5,23 @@
 #include <map>
 #include <new>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "gs_common.h"
 
 namespace gs {
 
 static thread_local std::string g_last_error;
+
+bool roctx_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GSYNC_ROCTX");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+void roctx_push(const char* name) { roctxRangePushA(name); }
+void roctx_pop() { roctxRangePop(); }
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
@@ -292,6 +304,7 @@ int gs_plan_set_ptrs(gs_plan* p, int slot, void* const* ptrs, void* /*stream*/) 
 
 int gs_pack(gs_plan* p, int src_slot, int src_dtype, void* flat, int flat_dtype, float scale,
             int scale_mode, void* stream) {
+  GsRange range("gs_pack");
   PLAN_OK(p);
   SLOT_OK(src_slot);
   GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_pack: NULL flat buffer");
@@ -302,6 +315,7 @@ int gs_pack(gs_plan* p, int src_slot, int src_dtype, void* flat, int flat_dtype,
 
 int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
               float* sqnorm_dev, int accumulate, void* stream) {
+  GsRange range("gs_unpack");
   PLAN_OK(p);
   SLOT_OK(dst_slot);
   GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_unpack: NULL flat buffer");
@@ -312,6 +326,7 @@ int gs_unpack(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int ds
 
 int gs_unpack_check(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, int dst_dtype,
                     float* found_inf, void* stream) {
+  GsRange range("gs_unpack_check");
   PLAN_OK(p);
   SLOT_OK(dst_slot);
   GS_CHECK_ARG(flat != nullptr || p->flat_numel == 0, "gs_unpack_check: NULL flat buffer");
@@ -321,6 +336,7 @@ int gs_unpack_check(gs_plan* p, const void* flat, int flat_dtype, int dst_slot, 
 }
 
 int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* stream) {
+  GsRange range("gs_scale");
   PLAN_OK(p);
   SLOT_OK(slot);
   GS_CHECK_ARG(scale_mode == GS_SCALE_MUL || scale_mode == GS_SCALE_DIV, "gs_scale: bad scale_mode");
@@ -329,11 +345,21 @@ int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* str
 }
 
 int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate, void* stream) {
+  GsRange range("gs_sqnorm");
   PLAN_OK(p);
   SLOT_OK(slot);
   GS_CHECK_ARG(sqnorm_dev != nullptr, "gs_sqnorm: NULL output");
   if (p->kind == GS_DEV_HOST) return host_sqnorm(p, slot, dtype, sqnorm_dev, accumulate);
   return hip_sqnorm(p, slot, dtype, sqnorm_dev, accumulate, stream);
+}
+
+int gs_sum(gs_plan* p, int slot, int dtype, float* sum_dev, int accumulate, void* stream) {
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(sum_dev != nullptr, "gs_sum: NULL output");
+  GsRange r("gs_sum");
+  if (p->kind == GS_DEV_HOST) return host_sum(p, slot, dtype, sum_dev, accumulate);
+  return hip_sum(p, slot, dtype, sum_dev, accumulate, stream);
 }
 
 int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,
@@ -356,6 +382,7 @@ int gs_adam_hyper(int device_kind, double* step, const double* lr, double beta1,
 
 int gs_unscale_check(gs_plan* p, int slot, int dtype, const float* inv_scale_dev,
                      float* found_inf_dev, void* stream) {
+  GsRange range("gs_unscale_check");
   PLAN_OK(p);
   SLOT_OK(slot);
   GS_CHECK_ARG(found_inf_dev != nullptr, "gs_unscale_check: NULL found_inf");
@@ -366,6 +393,7 @@ int gs_unscale_check(gs_plan* p, int slot, int dtype, const float* inv_scale_dev
 int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double momentum,
                 double dampening, double weight_decay, int nesterov, int maximize, int first_step,
                 const float* grad_scale_dev, const float* found_inf_dev, void* stream) {
+  GsRange range("gs_sgd_step");
   PLAN_OK(p);
   GS_CHECK_ARG(!nesterov || (momentum > 0 && dampening == 0),
                "Nesterov momentum requires a momentum and zero dampening");
@@ -384,6 +412,7 @@ int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double b
                  double beta2, double eps, double weight_decay, int adamw, int maximize,
                  double step_size, double bias_correction2_sqrt, const float* grad_scale_dev,
                  const float* found_inf_dev, void* stream) {
+  GsRange range("gs_adam_step");
   PLAN_OK(p);
   GS_CHECK_ARG(bias_correction2_sqrt > 0, "gs_adam_step: bias_correction2_sqrt must be > 0");
   AdamHyper h = make_adam(lr, beta1, beta2, eps, weight_decay, adamw, maximize, step_size,

@@ -30,6 +30,7 @@ backend and the collective is torch's gloo all-reduce.
 from __future__ import annotations
 
 import ctypes
+import os
 import sys
 from contextlib import contextmanager
 from typing import Any, Callable
@@ -191,19 +192,30 @@ class _Bucketer:
         members = [i for b in buckets for i in b]
         h = ctypes.c_void_p()
         comm = ddp._comm.handle if (ddp._comm is not None) else None
+        # torch buckets per dtype (compute_bucket_assignment_by_size keys on it):
+        # every bucket holds params of one dtype; its buffer has that dtype
+        # unless bucket_dtype overrides it
+        self.grad_dtypes = [params[b[0]].dtype for b in buckets]
+        self.bucket_dtypes = [ddp._bucket_dtype_override or gdt for gdt in self.grad_dtypes]
         L.check(
             L.lib().gs_bucketer_create(
                 comm, kind, ddp._dev_index, len(params), L.i64_array([p.numel() for p in params]),
-                L.gs_dtype(ddp._grad_dtype), len(buckets), L.i32_array(counts), L.i32_array(members),
-                L.gs_dtype(ddp._bucket_dtype), BUCKET_ALIGN_ELEMS, float(ddp.world_size), flags, ctypes.byref(h)),
+                L.gs_dtype(params[0].dtype), len(buckets), L.i32_array(counts), L.i32_array(members),
+                L.gs_dtype(ddp._bucket_dtype_override or params[0].dtype), BUCKET_ALIGN_ELEMS,
+                float(ddp.world_size), flags, ctypes.byref(h)),
             "gs_bucketer_create",
         )
         self.handle = h
         self.buffers = []
         for b in range(len(buckets)):
+            if any(params[i].dtype != self.grad_dtypes[b] for i in buckets[b]):
+                raise RuntimeError(f"bucket {b} mixes parameter dtypes")
+            L.check(L.lib().gs_bucketer_set_bucket_dtype(h, b, L.gs_dtype(self.grad_dtypes[b]),
+                                                         L.gs_dtype(self.bucket_dtypes[b])),
+                    "gs_bucketer_set_bucket_dtype")
             n = ctypes.c_int64()
             L.check(L.lib().gs_bucketer_bucket_numel(h, b, ctypes.byref(n)), "gs_bucketer_bucket_numel")
-            buf = torch.zeros(n.value, dtype=ddp._bucket_dtype, device=ddp.device)
+            buf = torch.zeros(n.value, dtype=self.bucket_dtypes[b], device=ddp.device)
             L.check(L.lib().gs_bucketer_set_bucket_buffer(h, b, buf.data_ptr()), "gs_bucketer_set_bucket_buffer")
             self.buffers.append(buf)
         self.loc = []
@@ -224,8 +236,8 @@ class _Bucketer:
 
     def logical_bytes(self):
         params = self.ddp._params
-        return [sum(params[i].numel() for i in b) * torch.tensor([], dtype=self.ddp._bucket_dtype).element_size()
-                for b in self.buckets]
+        return [sum(params[i].numel() for i in b) * torch.tensor([], dtype=dt).element_size()
+                for b, dt in zip(self.buckets, self.bucket_dtypes)]
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
@@ -288,9 +300,11 @@ class DistributedDataParallel(nn.Module):
         self.device_ids = device_ids if device_ids is None else [torch.device(d).index if not isinstance(d, int) else d for d in device_ids]
         self.output_device = output_device
         dtypes = {p.dtype for p in self._params}
-        if len(dtypes) != 1:
-            raise NotImplementedError(f"parameters of several dtypes are not supported yet: {dtypes}")
-        self._grad_dtype = next(iter(dtypes))
+        if not all(dt.is_floating_point for dt in dtypes):
+            raise NotImplementedError(f"gradient sync needs floating parameters, got {dtypes}")
+        # several dtypes -> buckets per dtype (torch's Reducer does the same)
+        self._bucket_dtype_override = bucket_dtype
+        self._grad_dtype = self._params[0].dtype if len(dtypes) == 1 else None
         self._bucket_dtype = bucket_dtype if bucket_dtype is not None else self._grad_dtype
         if self.device.type == "cuda":
             self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -310,6 +324,11 @@ class DistributedDataParallel(nn.Module):
         self._sqnorm_target: torch.Tensor | None = None
         self._found_inf_target: torch.Tensor | None = None
         self._found_inf_valid = False
+
+        # GSYNC_DEBUG=1: checksum every bucket before and after its collective
+        self._debug_sums = None
+        if os.environ.get("GSYNC_DEBUG", "0") not in ("", "0"):
+            self._debug_sums = torch.zeros(0)
 
         if init_sync:
             self._verify_param_shape_across_processes()
@@ -370,6 +389,9 @@ class DistributedDataParallel(nn.Module):
         t = getattr(self, "_found_inf_target", None)
         if t is not None:
             L.check(L.lib().gs_bucketer_set_found_inf(b.handle, t.data_ptr()), "gs_bucketer_set_found_inf")
+        if getattr(self, "_debug_sums", None) is not None:
+            self._debug_sums = torch.zeros(3 * len(buckets), dtype=torch.float32, device=self.device)
+            L.check(L.lib().gs_bucketer_set_debug(b.handle, self._debug_sums.data_ptr()), "gs_bucketer_set_debug")
         return b
 
     def _calib_allreduce(self, nbytes: int, iters: int = 4) -> float:
@@ -703,6 +725,52 @@ class DistributedDataParallel(nn.Module):
             out.append(ms.value)
         return out
 
+    def enable_bucket_checksums(self, on: bool = True):
+        """Debug mode (GSYNC_DEBUG=1 at construction does the
+        same): every synchronising backward writes Σ of each bucket after its
+        pack and after its collective (gs_bucketer_set_debug);
+        :meth:`verify_bucket_checksums` checks them across ranks."""
+        if on:
+            self._debug_sums = torch.zeros(3 * len(self._bucketer.buckets), dtype=torch.float32, device=self.device)
+            ptr = self._debug_sums.data_ptr()
+        else:
+            self._debug_sums, ptr = None, None
+        L.check(L.lib().gs_bucketer_set_debug(self._bucketer.handle, ptr), "gs_bucketer_set_debug")
+
+    def bucket_checksums(self):
+        """[(Σx after pack, Σx after collective, Σx² after pack)] per bucket of the last backward."""
+        if self._debug_sums is None or self._debug_sums.numel() == 0:
+            raise RuntimeError("bucket checksums are off (GSYNC_DEBUG=1 or enable_bucket_checksums())")
+        return [tuple(x) for x in self._debug_sums.view(-1, 3).cpu().tolist()]
+
+    def verify_bucket_checksums(self, rtol: float = 1e-4):
+        """Collective over the DDP group, after a synchronising backward:
+        * the all-reduced bucket is identical on every rank (Σx MIN == MAX);
+        * Σ_r (Σx after pack)_r == Σx after the collective within
+          rtol·sqrt(numel·Σ_r Σx²_r) (an fp32-rounding scale: >= rtol·Σ|x|/…
+          by Cauchy-Schwarz; a wrong or missing contribution is O(1) off).
+        Raises RuntimeError naming the first bad bucket; returns per bucket
+        (Σ_r pre, post, tolerance)."""
+        sums = self._debug_sums.view(-1, 3).double()
+        dev = self.device if self._backend == "nccl" else torch.device("cpu")
+        pre, post, sq = sums[:, 0].to(dev), sums[:, 1].to(dev), sums[:, 2].to(dev)
+        tot, sqt, lo, hi = pre.clone(), sq.clone(), post.clone(), post.clone()
+        dist.all_reduce(tot, group=self.process_group)
+        dist.all_reduce(sqt, group=self.process_group)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.process_group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.process_group)
+        out = []
+        for bi, buf in enumerate(self._bucketer.buffers):
+            tol = rtol * (buf.numel() * float(sqt[bi])) ** 0.5 + 1e-30
+            if float(lo[bi]) != float(hi[bi]):
+                raise RuntimeError(f"bucket {bi}: the all-reduced bucket differs across ranks "
+                                   f"(checksum {float(lo[bi])} vs {float(hi[bi])})")
+            if abs(float(tot[bi]) - float(post[bi])) > tol:
+                raise RuntimeError(f"bucket {bi}: sum over ranks of the packed bucket {float(tot[bi])} != "
+                                   f"the all-reduced bucket {float(post[bi])} (tolerance {tol})")
+            out.append((float(tot[bi]), float(post[bi]), tol))
+        return out
+
     def bucket_timeline_ms(self):
         """Per-bucket timeline of the last iteration (gs_bucketer_last_timing):
         list of dicts queue / pack / collective / unpack / ready_to_done, ms
@@ -743,7 +811,8 @@ class DistributedDataParallel(nn.Module):
             "bucket_sizes": b.logical_bytes(),
             "rebuilt_bucket_sizes": b.logical_bytes() if self._has_rebuilt_buckets else [],
             "padded_bucket_numels": [buf.numel() for buf in b.buffers],
-            "bucket_dtype": str(self._bucket_dtype),
+            "bucket_dtype": str(self._bucket_dtype) if self._bucket_dtype is not None else
+            ",".join(sorted({str(d) for d in b.bucket_dtypes})),
             "bucket_policy": self.bucket_policy,
             "last_bucket_cap_bytes": self._last_bucket_cap,
             "xgmi_calibration": self._xgmi_calibration,

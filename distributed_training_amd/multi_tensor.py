@@ -153,6 +153,14 @@ class TensorListPlan:
             "gs_sqnorm",
         )
 
+    def sum(self, slot, dtype, out: torch.Tensor, accumulate=False, stream=None):
+        """out[0] = Σ x over the slot's tensors (fp32, deterministic order)."""
+        L.check(
+            L.lib().gs_sum(self.handle, slot, L.gs_dtype(dtype), out.data_ptr(), int(bool(accumulate)),
+                           self._stream(stream)),
+            "gs_sum",
+        )
+
     def unscale_check(self, slot, dtype, inv_scale: torch.Tensor | None, found_inf: torch.Tensor, stream=None):
         L.check(
             L.lib().gs_unscale_check(self.handle, slot, L.gs_dtype(dtype),

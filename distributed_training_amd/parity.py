@@ -151,10 +151,21 @@ def ddp_parity_step(ddp, optimizer, run_forward_backward, k: int = 6) -> dict:
         cap = ddp._capture_local
         ddp._capture_local = None
     torch.cuda.synchronize(ddp.device) if ddp.device.type == "cuda" else None
-    local = torch.cat([cap[i].reshape(-1).float() for i in idx])
-    avg = torch.cat([params[i].grad.detach().reshape(-1).float() for i in idx])
-    gathered = coll.all_gather(local)
-    grads = compare_average(avg, gathered, coll.world, ddp._bucket_dtype)
+    # compare per bucket dtype (a model with params of several dtypes has buckets of each)
+    bucket_of = {i: b for b, members in enumerate(ddp._bucketer.buckets) for i in members}
+    by_dt: dict = {}
+    for i in idx:
+        by_dt.setdefault(ddp._bucketer.bucket_dtypes[bucket_of[i]], []).append(i)
+    parts = []
+    for dt, ids in by_dt.items():
+        local = torch.cat([cap[i].reshape(-1).float() for i in ids])
+        avg = torch.cat([params[i].grad.detach().reshape(-1).float() for i in ids])
+        parts.append(compare_average(avg, coll.all_gather(local), coll.world, dt))
+    grads = parts[0] if len(parts) == 1 else {
+        "elements": sum(p["elements"] for p in parts), "bitwise_equal": all(p["bitwise_equal"] for p in parts),
+        "max_abs_err": max(p["max_abs_err"] for p in parts),
+        "max_err_over_tol": max(p["max_err_over_tol"] for p in parts),
+        "tolerance": "; ".join(sorted({p["tolerance"] for p in parts})), "ok": all(p["ok"] for p in parts)}
     grads["checked_params"] = idx
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)

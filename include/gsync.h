@@ -169,6 +169,7 @@ int64_t gs_plan_task_units(gs_plan* p);
 #define GS_OP_UNSCALE 5
 #define GS_OP_SGD 6
 #define GS_OP_ADAM 7
+#define GS_OP_SUM 8
 int gs_plan_timer_enable(gs_plan* p, int n_slots);
 int gs_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap);
 /* register the per-tensor pointers of one slot (uploads on change, ordered on `stream`) */
@@ -197,6 +198,9 @@ int gs_scale(gs_plan* p, int slot, int dtype, float s, int scale_mode, void* str
 /* Σ x² over all tensors of one slot into sqnorm_dev[0] (fp32, deterministic order)
  * replaces: T:nn/utils/clip_grad.py:96 torch._foreach_norm (+ vector_norm of norms) */
 int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate, void* stream);
+/* Σ x over every tensor of a slot (fp32 accumulation, deterministic order):
+ * the bucket checksum of the GSYNC_DEBUG mode (gs_bucketer_set_debug) */
+int gs_sum(gs_plan* p, int slot, int dtype, float* sum_dev, int accumulate, void* stream);
 /* coef_dev[0] = min(1, max_norm / (sqrt(sqnorm_dev[0]) + eps)); norm_dev (nullable) = sqrt
  * replaces: T:nn/utils/clip_grad.py:165-174 clip_coef / clamp */
 int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,
@@ -288,7 +292,10 @@ int gs_bucketer_bucket_numel(gs_bucketer* b, int bucket, int64_t* out);
 /* padded numel of the reduce-scatter output shard for a bucket (ZeRO-2) */
 int gs_bucketer_shard_numel(gs_bucketer* b, int bucket, int64_t* out);
 int gs_bucketer_param_location(gs_bucketer* b, int param, int32_t* bucket, int64_t* offset);
-/* storage for bucket `bucket` (torch-owned, bucket_numel elements of bucket_dtype) */
+/* per-bucket dtypes (torch's Reducer buckets per dtype: a model with params of
+ * several floating dtypes gets buckets of each; create() sets the defaults) */
+int gs_bucketer_set_bucket_dtype(gs_bucketer* b, int bucket, int grad_dtype, int bucket_dtype);
+/* storage for bucket `bucket` (torch-owned, bucket_numel elements of its bucket dtype) */
 int gs_bucketer_set_bucket_buffer(gs_bucketer* b, int bucket, void* ptr);
 /* ZeRO-2 output shard storage for bucket */
 int gs_bucketer_set_shard_buffer(gs_bucketer* b, int bucket, void* ptr);
@@ -321,6 +328,16 @@ int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
  *   out[4] ready -> every bucket finished (the finalize event): for the last
  *          bucket this is the exposed end-of-backward tail */
 int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out /* [5] */);
+/* Debug mode (checksum each bucket before and after the
+ * collective): with a non-NULL device (host, for host buckets) buffer of
+ * 3 * n_buckets floats, every backward writes sums[3b] = Σx of bucket b after
+ * its pack (before the collective), sums[3b+1] = Σx after the collective
+ * (before the unpack) and sums[3b+2] = Σx² after the pack.  Across ranks
+ * Σ_r sums_r[3b] must equal sums[3b+1] up to fp32 rounding and sums[3b+1]
+ * must be identical on every rank
+ * (distributed_training_amd.ddp.DistributedDataParallel.verify_bucket_checksums).
+ * NULL disables. */
+int gs_bucketer_set_debug(gs_bucketer* b, float* sums);
 
 /* ====================================================================
  * Input step of the CIFAR configuration

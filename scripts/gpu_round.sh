@@ -39,17 +39,24 @@ if [ "${PROFILE:-0}" == "1" ]; then
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o bench -- python3 -u bench.py --gpus 1 --steps 5 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
   find $OUT/prof_$TAG -name "*stats*"
   python3 scripts/overlap.py $(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1) $OUT/overlap_$TAG.json > /dev/null || true
+  # keep the summaries (gpurun copies back <= 64 MiB): drop the full traces
+  for f in $(find $OUT/prof_$TAG -name "*stats*.csv"); do cp $f $OUT/${TAG}_$(basename $f); done
+  rm -rf $OUT/prof_$TAG
+fi
+if [ "${KBENCH:-0}" == "1" ]; then
+  echo "== kernel microbench (bench_kernels, R50 and R152x2 > Infinity Cache)"
+  timeout -k 10 300 python -u bench_kernels.py --model resnet50 --replicas 1 --iters 50 > $OUT/${TAG}_kernels_resnet50.jsonl 2> $OUT/${TAG}_kb.err || { tail $OUT/${TAG}_kb.err; exit 1; }
+  timeout -k 10 300 python -u bench_kernels.py --model resnet152 --replicas 2 --iters 50 > $OUT/${TAG}_kernels_resnet152x2.jsonl 2>> $OUT/${TAG}_kb.err || { tail $OUT/${TAG}_kb.err; exit 1; }
 fi
 if [ "${PMC:-0}" == "1" ]; then
-  echo "== PMC traffic (separate passes)"
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 > $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_$TAG -o sgd -- python3 scripts/sgd_only.py resnet50 10 >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
-  python3 scripts/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG resnet50/sgd $OUT/pmc_traffic_$TAG.json
-  for mo in ${PMC_EXTRA:-}; do  # e.g. PMC_EXTRA="resnet50:adam resnet152:sgd"
-    m=${mo%%:*}; o=${mo#*:}
-    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_${TAG}_${m}_$o -o k -- python3 scripts/sgd_only.py $m 10 $o >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
-    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_${TAG}_${m}_$o -o k -- python3 scripts/sgd_only.py $m 10 $o >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+  echo "== PMC traffic (separate FETCH_SIZE / WRITE_SIZE passes per kernel)"
+  for mo in ${PMC_OPS:-resnet50:sgd resnet50:adam resnet50:pack resnet50:pack16 resnet50:unpack resnet50:sqnorm resnet50:unpacksq resnet152:sgd resnet152x2:pack resnet152x2:unpack resnet152x2:sqnorm}; do
+    m=${mo%%:*}; o=${mo#*:}; reps=1; mm=$m
+    case $m in *x2) mm=${m%x2}; reps=2;; esac
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc_fetch_${TAG}_${m}_$o -o k -- python3 scripts/kernel_only.py $mm 10 $o $reps >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc_write_${TAG}_${m}_$o -o k -- python3 scripts/kernel_only.py $mm 10 $o $reps >> $OUT/pmc_$TAG.log 2>&1 || { tail $OUT/pmc_$TAG.log; exit 1; }
     python3 scripts/pmc_traffic.py $OUT/pmc_fetch_${TAG}_${m}_$o $OUT/pmc_write_${TAG}_${m}_$o $m/$o $OUT/pmc_traffic_$TAG.json
+    rm -rf $OUT/pmc_fetch_${TAG}_${m}_$o $OUT/pmc_write_${TAG}_${m}_$o
   done
 fi
 echo "== done"

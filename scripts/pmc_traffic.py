@@ -1,5 +1,5 @@
 """Turn rocprofv3 --pmc CSVs (separate FETCH_SIZE and WRITE_SIZE passes) into
-per-launch HBM bytes for the fused SGD kernel, with the gfx950 correction of
+per-launch HBM bytes for one grad-sync kernel (scripts/kernel_only.py), with the gfx950 correction of
 MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half the bytes of wide (16 B/lane)
 coalesced streaming reads -> x2; WRITE_SIZE is exact for 16-B stores.
 Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <key> <out.json>"""
@@ -10,7 +10,8 @@ import os
 import sys
 
 
-KERNEL = {"sgd": "SgdOp", "adam": "AdamOp"}
+KERNEL = {"sgd": "SgdOp", "adam": "AdamOp", "pack": "PackOp", "pack16": "PackOp", "unpack": "UnpackOp",
+          "unpacksq": "UnpackOp", "sqnorm": "SqnormOp"}
 
 
 def load(d, counter, tag="SgdOp"):

@@ -72,8 +72,8 @@ def _ds_run(rank, ws, stage, bf16):
         assert torch.isfinite(loss.float()).item()
         if i == 2:
             break
-    # WarmupLR: log ramp from 0 toward 1e-3
-    assert lrs[0] > 0 and lrs[0] < lrs[1] < lrs[2] < 1e-3
+    # WarmupLR (DeepSpeed schedule): the lr after steps 1..3 is gamma(0) = 0, gamma(1), gamma(2)
+    assert lrs[0] == 0.0 and 0 < lrs[1] < lrs[2] < 1e-3
     changed = sum(int(not torch.equal(a, b)) for a, b in zip(before, model.parameters()))
     assert changed > 0
     w = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
@@ -133,3 +133,28 @@ def _col_run(rank, ws, plugin_name, mp):
 @pytest.mark.parametrize("plugin,mp", [("torch_ddp", None), ("torch_ddp", "bf16"), ("low_level_zero", None)])
 def test_colossal_shim(plugin, mp):
     _run(_col_run, 2, plugin, mp)
+
+
+def test_warmup_lr_schedule_matches_deepspeed():
+    """DeepSpeed WarmupLR (R:resnet/deepspeed/deepspeed_train.py:187-194): the lrs
+    the first three optimizer steps run with are [min, min, min + (max-min)*log2/logN]
+    (construction sets min; each scheduler.step() after an optimizer step
+    advances last_batch_iteration and sets gamma(last_batch_iteration))."""
+    import math
+
+    sys.path.insert(0, SHIMS)
+    from distributed_training_amd.compat.deepspeed import WarmupLR
+
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=123.0)
+    sch = WarmupLR(opt, warmup_min_lr=0.0, warmup_max_lr=1e-3, warmup_num_steps=1000)
+    used = []
+    for _ in range(4):
+        used.append(opt.param_groups[0]["lr"])  # the lr this optimizer step runs with
+        sch.step()
+    assert used[0] == 0.0 and used[1] == 0.0
+    assert abs(used[2] - 1e-3 * math.log(2) / math.log(1000)) < 1e-15
+    assert abs(used[3] - 1e-3 * math.log(3) / math.log(1000)) < 1e-15
+    assert sch.get_lr()[0] == opt.param_groups[0]["lr"]
+    sch2 = WarmupLR(opt, warmup_min_lr=0.0, warmup_max_lr=1e-3, warmup_num_steps=1000)
+    sch2.load_state_dict(sch.state_dict())
+    assert opt.param_groups[0]["lr"] == sch.get_lr()[0]

@@ -228,7 +228,8 @@ def test_ddp_ws2_one_gpu_gloo_collective(cuda_device):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
 
-@pytest.mark.parametrize("mode", ["no_sync", "view", "small_buckets", "find_unused", "bf16_model"])
+@pytest.mark.parametrize("mode", ["no_sync", "view", "small_buckets", "find_unused", "bf16_model", "mixed_dtype",
+                                  "debug_checksums", "last_bucket_cap"])
 def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
     """torch-DDP options on the RCCL path; at ws=1 the averaged grad must equal
     the (accumulated) local grad bit for bit."""
@@ -244,8 +245,18 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
         def forward(self, x):
             return self.body(x)
 
+    class Mixed(torch.nn.Module):  # fp32 body, bf16 head: per-dtype buckets
+        def __init__(self):
+            super().__init__()
+            self.body = micro_resnet()
+            self.head = torch.nn.Linear(10, 5).to(torch.bfloat16)
+
+        def forward(self, x):
+            return self.head(self.body(x).to(torch.bfloat16)).float()
+
     torch.manual_seed(0)
-    model = (WithUnused() if mode == "find_unused" else micro_resnet()).to(cuda_device)
+    model = (WithUnused() if mode == "find_unused" else Mixed() if mode == "mixed_dtype" else micro_resnet())
+    model = model.to(cuda_device)
     if mode == "bf16_model":
         model = model.to(torch.bfloat16)
     params = list(model.parameters())
@@ -254,7 +265,11 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
     kw = {"find_unused_parameters": mode == "find_unused", "gradient_as_bucket_view": mode == "view"}
     if mode == "small_buckets":
         kw["bucket_cap_mb"] = 0.02
+    if mode == "last_bucket_cap":
+        kw["last_bucket_cap_mb"] = 0.001
     ddp = DistributedDataParallel(model, **kw)
+    if mode == "debug_checksums":
+        ddp.enable_bucket_checksums()
     dt = torch.bfloat16 if mode == "bf16_model" else torch.float32
     g = torch.Generator(device=cuda_device).manual_seed(3)
     for it in range(3):
@@ -266,6 +281,11 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
                     ddp(x).float().sum().backward()
         ddp(xs[2]).float().sum().backward()
         torch.cuda.synchronize()
+        if mode == "debug_checksums":
+            for tot, post, tol in ddp.verify_bucket_checksums():
+                assert tot == post  # ws=1: the collective is the identity
+        if mode == "mixed_dtype":
+            assert set(ddp._bucketer.bucket_dtypes) == {torch.float32, torch.bfloat16}
         for i, p in enumerate(params):
             if mode == "find_unused" and i >= len(params) - 2:
                 assert p.grad is None
@@ -279,6 +299,11 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
             ddp.zero_grad(set_to_none=True)
     if mode == "small_buckets":
         assert len(ddp.bucket_indices()) > 3
+    if mode == "last_bucket_cap":
+        last = ddp.bucket_indices()[-1]
+        assert len(last) == 1 or sum(params[i].numel() * 4 for i in last) <= 1048
+        t = ddp.tail_ms()
+        assert t is not None and t["total"] >= t["pack"] >= 0
 
 
 def test_communicator_watchdog_and_abort(cuda_device):

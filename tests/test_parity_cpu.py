@@ -163,3 +163,47 @@ def _policy_grads(rank, ws):
 
 def test_bucket_policies_change_no_sum():
     _run(_policy_grads, 2)
+
+
+def _debug_checksums(rank, ws, corrupt):
+    import os
+
+    os.environ["GSYNC_DEBUG"] = "1"
+    import distributed_training_amd as D
+
+    torch.manual_seed(0)
+    model = _micro()
+    ddp = D.DistributedDataParallel(model)
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.rand(4, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (4,), generator=g)
+    for it in range(3):  # iteration 0: one bucket; then the rebuilt layout
+        if it == 2 and corrupt and rank == 1:
+            inner = ddp._launch_external
+
+            def bad(bucket_ids, inner=inner):
+                for bi in bucket_ids:
+                    if corrupt == "before":
+                        ddp._bucketer.buffers[bi].add_(1.0)  # a wrong contribution enters the sum
+                inner(bucket_ids)
+                if corrupt == "after":
+                    for bi in bucket_ids:
+                        ddp._pending[bi][1].wait()
+                        ddp._bucketer.buffers[bi].add_(1.0)  # one rank's result diverges
+            ddp._launch_external = bad
+        for p in model.parameters():
+            p.grad = None
+        torch.nn.functional.cross_entropy(ddp(x), y).backward()
+        sums = ddp.bucket_checksums()
+        assert len(sums) == len(ddp.bucket_indices())
+        if it < 2 or not corrupt:
+            out = ddp.verify_bucket_checksums()
+            assert all(abs(t - p) <= tol for t, p, tol in out)
+        else:
+            with pytest.raises(RuntimeError, match="bucket"):
+                ddp.verify_bucket_checksums()
+
+
+@pytest.mark.parametrize("corrupt", [None, "before", "after"])
+def test_debug_bucket_checksums(corrupt):
+    _run(_debug_checksums, 2, corrupt)
