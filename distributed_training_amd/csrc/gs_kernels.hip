@@ -1070,7 +1070,11 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     if (Op::kRed != 0 && red_out && !accumulate) HIP_RET(hipMemsetAsync(red_out, 0, 4, s));
     return GS_OK;
   }
-  GS_TRY_RET(hip_plan_flush(p, stream));
+  {
+    GsRange r("gs_plan_flush");
+    GS_TRY_RET(hip_plan_flush(p, stream));
+  }
+  GsRange r_launch("gs_kernel_launch");
   op.partials = p->d_partials;
   const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
