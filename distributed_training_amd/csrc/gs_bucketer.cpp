@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <functional>
 #include <mutex>
 
@@ -83,7 +84,10 @@ struct gs_bucketer {
   float* dbg = nullptr;        // GSYNC_DEBUG: [3 * n_buckets] Σx after pack, Σx after collective, Σx² after pack
   void* producer = nullptr;
   hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_comm = nullptr;     // comm stream's earlier buckets, joined before a producer-side tail
   bool done_timed = false;
+  bool tail_on_producer = true;     // GSYNC_TAIL_ON_PRODUCER=0 keeps every bucket on the comm stream
+  bool tail_ran_on_producer = false;
   std::mutex mu;
 
   bool hip() const { return kind == GS_DEV_HIP; }
@@ -186,9 +190,24 @@ int launch_bucket(gs_bucketer* b, int bi) {
   if (!b->hip()) {
     GS_TRY_RET(pack_one(b, bk, nullptr));
   } else if (b->auto_coll()) {
-    hipStream_t cs = comm_stream(b->comm);
-    HIPB_RET(hipEventRecord(bk.ev_ready, static_cast<hipStream_t>(b->producer)));
-    HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
+    // The last bucket's chain is the exposed end-of-backward tail: nothing is
+    // left to overlap it with, so it runs on the producer stream itself — no
+    // cross-stream hop to start it (its "queue") and none back at finalize.
+    // The producer first joins the comm stream's earlier buckets, so the
+    // communicator's collectives stay in issue order on the GPU.
+    const bool on_producer = b->tail_on_producer && bi == static_cast<int>(b->buckets.size()) - 1;
+    hipStream_t ps = static_cast<hipStream_t>(b->producer);
+    hipStream_t cs = on_producer ? ps : comm_stream(b->comm);
+    HIPB_RET(hipEventRecord(bk.ev_ready, ps));
+    if (on_producer) {
+      if (bi > 0) {
+        HIPB_RET(hipEventRecord(b->ev_comm, comm_stream(b->comm)));
+        HIPB_RET(hipStreamWaitEvent(ps, b->ev_comm, 0));
+      }
+      b->tail_ran_on_producer = true;
+    } else {
+      HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
+    }
     // timing events stay out of a hipGraph capture (last_comm_ms then reports -1)
     const bool timed = !stream_capturing(cs);
     if (timed) HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
@@ -296,7 +315,13 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
   for (int p = 0; p < n_params; ++p)
     if (b->loc_bucket[p] < 0)
       return bail(fail(GS_EINVAL, "gs_bucketer_create: parameter " + std::to_string(p) + " is in no bucket"));
-  if (device_kind == GS_DEV_HIP && hipEventCreate(&b->ev_done) != hipSuccess)
+  {
+    const char* e = std::getenv("GSYNC_TAIL_ON_PRODUCER");
+    b->tail_on_producer = !(e && std::atoi(e) == 0);
+  }
+  if (device_kind == GS_DEV_HIP &&
+      (hipEventCreateWithFlags(&b->ev_comm, hipEventDisableTiming) != hipSuccess ||
+       hipEventCreate(&b->ev_done) != hipSuccess))
     return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
   *out = b;
   return GS_OK;
@@ -312,6 +337,7 @@ int gs_bucketer_destroy(gs_bucketer* b) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (b->ev_done) (void)hipEventDestroy(b->ev_done);
+  if (b->ev_comm) (void)hipEventDestroy(b->ev_comm);
   delete b;
   return GS_OK;
 }
@@ -373,6 +399,7 @@ int gs_bucketer_prepare(gs_bucketer* b, float* sqnorm_dev) {
     bk.unpacked = false;
   }
   b->next_bucket = 0;
+  b->tail_ran_on_producer = false;
   b->prepared = true;
   b->sqnorm = sqnorm_dev;
   b->sq_count = 0;
@@ -430,10 +457,18 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
                 "one. Parameter indices which did not receive grad: " + missing);
   }
   if (b->hip() && b->auto_coll()) {
-    hipStream_t cs = comm_stream(b->comm);
-    HIPB_RET(hipEventRecord(b->ev_done, cs));
-    b->done_timed = !stream_capturing(cs);
-    HIPB_RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), b->ev_done, 0));
+    hipStream_t ps = static_cast<hipStream_t>(stream);
+    if (b->tail_ran_on_producer && ps == static_cast<hipStream_t>(b->producer)) {
+      // the last bucket ran on the producer after joining the comm stream:
+      // everything is already ordered before this point
+      HIPB_RET(hipEventRecord(b->ev_done, ps));
+      b->done_timed = !stream_capturing(ps);
+    } else {
+      hipStream_t cs = comm_stream(b->comm);
+      HIPB_RET(hipEventRecord(b->ev_done, cs));
+      b->done_timed = !stream_capturing(cs);
+      HIPB_RET(hipStreamWaitEvent(ps, b->ev_done, 0));
+    }
   } else {
     // external collectives (comm hook / process group) are done by now
     for (Bucket& bk : b->buckets) {

@@ -601,7 +601,7 @@ template <class Op>
 __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, Op op) {
   static_assert(Op::kN == kUnit, "the chunk engine moves 4 elements per lane-access");
   constexpr int G = Op::kG;
-  static_assert(G == 1 || G == 2 || G == 4, "group of 1, 2 or 4 chunks");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "group of 1, 2, 4 or 8 chunks");
   float acc = 0.f;
   if (!op.active()) return;  // uniform across the grid
   load_hyper(op);            // uniform: graph-replayable lr / bias corrections

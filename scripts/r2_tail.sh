@@ -1,34 +1,22 @@
 #!/bin/bash
-# Host-side enqueue ranges of the bucket path (roctx marker trace, summaries
-# only) and the exposed tail with / without a capped last bucket (N=1).
+# The exposed end-of-backward tail, A/B: the last bucket's chain on the
+# producer stream (default) vs on the comm stream (GSYNC_TAIL_ON_PRODUCER=0),
+# with and without a 1 MiB last bucket; GPU tests of the paths it touches first.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-TAG=${TAG:-r2i}
+TAG=${TAG:-r2k}
 export TMPDIR=/tmp
-echo "== roctx marker trace"
-GSYNC_ROCTX=1 timeout -k 10 600 rocprofv3 --marker-trace --stats -f csv -d $OUT/mk_$TAG -o bench -- python3 -u bench.py --steps 3 --warmup 2 --cpu-baseline 0 --parity 0 > $OUT/${TAG}_marker_bench.json 2> $OUT/${TAG}_marker.err || { tail -20 $OUT/${TAG}_marker.err; exit 1; }
-python3 - $OUT/mk_$TAG $OUT/${TAG}_marker_ranges.json <<'PY'
-import csv, glob, json, os, sys, collections
-rows = []
-for f in glob.glob(os.path.join(sys.argv[1], "**", "*marker_api_trace.csv"), recursive=True):
-    rows += list(csv.DictReader(open(f)))
-agg = collections.defaultdict(list)
-for r in rows:
-    name = r.get("Function") or r.get("Name") or "?"
-    try:
-        agg[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    except Exception:
-        pass
-out = {k: {"count": len(v), "host_us_total": sum(v), "host_us_max": max(v), "host_us_median": sorted(v)[len(v) // 2]}
-       for k, v in sorted(agg.items())}
-json.dump(out, open(sys.argv[2], "w"), indent=1)
-print(json.dumps(out))
-PY
-rm -rf $OUT/mk_$TAG
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ddp.py tests/test_gpu_zero.py tests/test_gpu_graphs.py tests/test_gpu_amp_nosync.py -x -q --timeout 200 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1 || { tail -30 $OUT/${TAG}_tests.log; exit 1; }
+tail -1 $OUT/${TAG}_tests.log
+for tp in 1 0; do
 for cap in none 1; do
-  echo "== bench last-bucket cap $cap"
+  echo "== bench tail_on_producer=$tp last-bucket cap $cap"
   extra=""; [ $cap != none ] && extra="--last-bucket-cap-mb $cap"
-  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --cpu-baseline 0 $extra > $OUT/${TAG}_bench_cap_$cap.json 2> $OUT/${TAG}_bench_cap_$cap.err || { tail -20 $OUT/${TAG}_bench_cap_$cap.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$OUT/${TAG}_bench_cap_$cap.json')); print(d['value'], d['ms_per_step'], d['grad_sync']['tail_ms'], d['grad_sync']['bucket_bytes'], d['parity']['ok'])"
+  GSYNC_TAIL_ON_PRODUCER=$tp timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --cpu-baseline 0 --kernel-rates 0 $extra > $OUT/${TAG}_bench_tp${tp}_cap_$cap.json 2> $OUT/${TAG}_bench_tp${tp}_cap_$cap.err || { tail -20 $OUT/${TAG}_bench_tp${tp}_cap_$cap.err; exit 1; }
+  python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/${TAG}_bench_tp${tp}_cap_$cap.json') if l.startswith('{')][0]
+print(round(d['value'],1), round(d['ms_per_step'],3), d['grad_sync']['tail_ms'], d['parity']['ok'])"
+done
 done

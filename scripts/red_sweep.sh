@@ -11,8 +11,8 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 
 tail -1 $OUT/${TAG}_tests.log
 for m in "resnet50 1" "resnet152 2"; do
   set -- $m
-  for grid in 2048 8192 65536; do
-    for lib in default gred4; do
+  for grid in ${GRIDS:-2048 8192 65536}; do
+    for lib in ${LIBS:-default gred4}; do
       L=distributed_training_amd/lib/libgsync.so; [ $lib != default ] && L=distributed_training_amd/lib/variants/libgsync_$lib.so
       GSYNC_LIB=$L GS_RED_GRID=$grid timeout -k 10 300 python -u bench_kernels.py --model $1 --replicas $2 --skip-torch --iters 50 --tag g${grid}_$lib >> $J 2> $OUT/${TAG}_bk.err || { tail -20 $OUT/${TAG}_bk.err; exit 1; }
     done

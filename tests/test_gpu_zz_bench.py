@@ -63,6 +63,12 @@ def _check_line(d, n):
     g = d["grad_sync"]
     assert g["n_buckets"] == len(g["bucket_bytes"]) >= 1
     assert g["grad_bytes_per_step"] == 4 * d["config"]["params"]
+    # every grad-sync kernel alone on the model's params (the north star's >= 70 % covers them all)
+    k = d["grad_sync_kernels"]
+    assert set(k["kernels"]) == {"pack_f32", "pack_f32_to_bf16", "unpack_f32", "unpack_f32+sqnorm", "sqnorm_f32",
+                                 "sgd_momentum_wd", "adam"}
+    assert all(r["GBps"] > 0 and abs(r["frac"] - r["GBps"] / 8000.0) < 1e-12 for r in k["kernels"].values())
+    assert k["params"] == d["config"]["params"]
     # the self-check step after the timed region (distributed_training_amd/parity.py)
     p = d["parity"]
     assert p is not None and p["ok"] is True and p["world"] == n, p
