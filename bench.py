@@ -53,8 +53,10 @@ def parse():
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--bucket-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam"])
-    ap.add_argument("--engine", default="ddp", choices=["ddp", "zero1", "zero2"],
-                    help="ddp = headline (BASELINE configs[1-2]); zero1/zero2 = DeepSpeed-style (configs[3])")
+    ap.add_argument("--engine", default="ddp", choices=["ddp", "zero1", "zero2", "colossal"],
+                    help="ddp = headline (BASELINE configs[1-2]); zero1/zero2 = DeepSpeed-style (configs[3]); "
+                         "colossal = the Colossal Booster shim as run.sh drives it (TorchDDPPlugin, fp16 mixed "
+                         "precision, HybridAdam; configs[4] with --model resnet152)")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--grad-as-bucket-view", action="store_true",
                     help="DDP(gradient_as_bucket_view=True): grads alias the buckets, no unpack pass")
@@ -266,6 +268,18 @@ def main():
             opt = D.FusedAdam(ddp.parameters(), lr=1e-3 * world, capturable=bool(args.graph))
             bytes_per_param = 28
         grad_bytes = n_params * (2 if bucket_dtype is not None else 4)
+    elif args.engine == "colossal":
+        # BASELINE configs[4] through the Colossal shim exactly as R:resnet/colossal/run.sh drives it:
+        # TorchDDPPlugin + mixed_precision='fp16' + HybridAdam(lr=1e-3*ws) (R:colossal_train.py:118-161);
+        # fp32 params and grads, libgsync DDP underneath, GradScaler's check fused into the unpack
+        from distributed_training_amd.compat import colossalai as C
+
+        booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
+        opt = C.HybridAdam(model.parameters(), lr=1e-3 * world)
+        cmodel, opt_w, ccrit, _, _ = booster.boost(model, opt, criterion=torch.nn.CrossEntropyLoss())
+        ddp = cmodel.module  # _AutocastModule(libgsync DDP)
+        bytes_per_param = 28
+        grad_bytes = n_params * 4
     else:
         # DeepSpeed-style ZeRO (BASELINE configs[3]): bf16 model, fp32 master shard,
         # reduce-scatter (zero2) / all-reduce (zero1) of bf16 grads, AdamW, all-gather
@@ -316,7 +330,14 @@ def main():
             opt.zero_grad(set_to_none=True)
         return loss
 
-    run = train_step
+    def colossal_step(xb, yb):  # R:resnet/colossal/colossal_train.py:97-102
+        loss = ccrit(cmodel(xb), yb)
+        booster.backward(loss, opt_w)
+        opt_w.step()
+        opt_w.zero_grad()
+        return loss
+
+    run = colossal_step if args.engine == "colossal" else train_step
     if args.graph:
         if zero is not None:
             raise SystemExit("--graph: DDP engine only")
@@ -368,7 +389,14 @@ def main():
     if args.parity and args.impl == "libgsync" and not args.graph:
         from distributed_training_amd import parity as PC
 
-        if zero is None:
+        if zero is None and args.engine == "colossal":
+            def fwd_bwd():
+                booster.backward(ccrit(cmodel(x), y), opt_w)
+
+            opt_ms_saved = opt.kernel_ms()
+            parity = PC.ddp_parity_step(ddp, opt_w, fwd_bwd)
+            opt.kernel_ms()
+        elif zero is None:
             def fwd_bwd():
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     loss = crit(ddp(x), y)
@@ -470,12 +498,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp16" if args.engine == "colossal" else "bf16",
         "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
         "config": {
             "workload": (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
                          f"REFERENCE PATH torch DDP + torch.optim.{'SGD' if args.optimizer == 'sgd' else 'Adam'}"
                          f"(foreach) for comparison") if args.impl == "torch" else
+                        (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, Colossal "
+                         f"Booster(TorchDDPPlugin, mixed_precision='fp16') + HybridAdam as R:resnet/colossal/run.sh: "
+                         f"libgsync DDP (fp32 buckets, GradScaler inf check fused into the unpack) + fused Adam") if
+                        args.engine == "colossal" else
                         (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
                          f"{'one hipGraph per step: ' if args.graph else ''}libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
                          f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}") if zero is None else
@@ -498,7 +530,9 @@ def main():
             "params": n_params,
         },
         "roofline": None if args.impl == "torch" else {
-            "kernel": (f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
+            "kernel": ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
+                       if args.engine == "colossal" else
+                       f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)")
                        if zero is None else
                        f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> + bf16 param write)"),
             "bound": "hbm",

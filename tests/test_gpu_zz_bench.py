@@ -102,3 +102,16 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     _check_line(lines[0], 2)
     assert "rehearsal" in lines[0]["config"]
     assert lines[0]["parity"]["collective"] == "gloo"
+
+
+def test_bench_colossal_engine(cuda_device):
+    """BASELINE configs[4]'s path: the Colossal Booster shim as run.sh drives it
+    (TorchDDPPlugin, fp16 mixed precision, HybridAdam) through bench.py."""
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1", "--engine", "colossal", "--kernel-rates", "0"]
+                       + SMALL, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _json_lines(p.stdout)[0]
+    assert d["config"]["engine"] == "colossal" and d["dtype"] == "fp16"
+    assert d["roofline"]["algorithmic_bytes_per_launch"] == 28 * d["config"]["params"]
+    assert d["roofline"]["launches"] == 3 and d["roofline"]["achieved"] > 0
+    assert d["parity"]["ok"] is True and d["parity"]["averaged_grads"]["bitwise_equal"] is True
