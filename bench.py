@@ -532,9 +532,11 @@ def main():
         "roofline": None if args.impl == "torch" else {
             "kernel": ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
                        if args.engine == "colossal" else
-                       f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)")
+                       f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update "
+                       f"(chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
                        if zero is None else
-                       f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> + bf16 param write)"),
+                       f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> "
+                       f"+ bf16 param write)"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
