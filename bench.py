@@ -370,12 +370,31 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.pg_backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
-    tail = timeline = None
-    if zero is None and args.impl == "libgsync":
-        comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # last iteration, per bucket (HIP events on the comm stream)
-        if not args.graph:
-            tail = ddp.tail_ms()  # last timed step: last bucket ready -> all bucket chains done
-            timeline = ddp.bucket_timeline_ms()
+    # the timed launches' kernel durations, read before any untimed step below adds more
+    opt_ms_saved = zero_ms_saved = None
+    if args.impl == "libgsync" and not args.graph:
+        if zero is None:
+            opt_ms_saved = opt.kernel_ms()
+        else:
+            from distributed_training_amd import _lib as L
+
+            zero_ms_saved = zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM)
+    tail = timeline = tail_timed = None
+    if zero is None and args.impl == "libgsync" and not args.graph:
+        # timed steps ran at timeline level 1: two events per step, the tail total
+        # (last bucket ready -> every bucket chain done) of the last timed step
+        tail_timed = ddp.tail_ms()
+        # the split (queue / pack / collective / unpack per bucket) needs ~4 events a
+        # bucket, ~10 µs each on the exposed tail: read it from untimed steps at level 2
+        ddp.set_timeline(2)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # per bucket, HIP events on the comm stream
+        tail = ddp.tail_ms()
+        timeline = ddp.bucket_timeline_ms()
+        ddp.set_timeline(1)
+        opt.kernel_ms()  # drop the untimed steps' launches
 
     coll = None
     if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
@@ -393,25 +412,18 @@ def main():
             def fwd_bwd():
                 booster.backward(ccrit(cmodel(x), y), opt_w)
 
-            opt_ms_saved = opt.kernel_ms()
             parity = PC.ddp_parity_step(ddp, opt_w, fwd_bwd)
-            opt.kernel_ms()
         elif zero is None:
             def fwd_bwd():
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     loss = crit(ddp(x), y)
                 loss.backward()
 
-            opt_ms_saved = opt.kernel_ms()  # the timed launches, read before the check step adds one
             parity = PC.ddp_parity_step(ddp, opt, fwd_bwd)
-            opt.kernel_ms()
         else:
             def fwd_bwd():
                 crit(ddp(x).float(), y).backward()
 
-            from distributed_training_amd import _lib as L
-
-            zero_ms_saved = zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM)
             parity = PC.zero_parity_step(zero, fwd_bwd)
         if rank == 0:
             print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
@@ -429,14 +441,11 @@ def main():
     elif zero is None:
         # update-kernel launches, HIP events recorded by libgsync on the launch stream
         # right around each kernel (the pointer-table upload, if any, stays outside)
-        opt_ms = sorted(opt_ms_saved if parity is not None else opt.kernel_ms())
+        opt_ms = sorted(opt_ms_saved)
     else:
         # the fused shard update alone (plan launch timer); the whole zero.step() window
         # (norm, clip, update, all-gather) is reported beside it
-        from distributed_training_amd import _lib as L
-
-        opt_ms = sorted(zero_ms_saved if parity is not None else
-                        zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM))
+        opt_ms = sorted(zero_ms_saved)
         win_ms = sorted(a.elapsed_time(b) for a, b in ev_opt)
     opt_ms_avg = sum(opt_ms) / len(opt_ms) if opt_ms else None
     img_s = world * args.batch * args.steps / elapsed
@@ -476,11 +485,15 @@ def main():
         grad_sync.update({"allreduce_ms_per_step": tot_ms, "allreduce_bus_GBps": bus, "xgmi_peak_GBps": peak,
                           "frac": bus / peak, "per_bucket_ms": comm_ms,
                           "note": "in-step: HIP events around each bucket collective on the comm stream, "
-                                  "last timed step, includes cross-rank arrival skew under backward"})
+                                  "an untimed step after the timed region (timeline level 2), includes "
+                                  "cross-rank arrival skew under backward"})
     if coll is not None:
         grad_sync["standalone"] = coll
     if tail is not None:
-        grad_sync["tail_ms"] = tail
+        # total: the last TIMED step (2 events a step); the split: an untimed step with
+        # every bucket's events (they stretch that step's tail by ~10 µs each)
+        grad_sync["tail_ms"] = dict(tail, total_timed_step=tail_timed["total"] if tail_timed else None,
+                                    split_from="untimed step at timeline level 2")
         grad_sync["bucket_timeline_ms"] = timeline
     if zero is None and args.impl == "libgsync":
         grad_sync["bucket_policy"] = log.get("bucket_policy")

@@ -57,7 +57,9 @@ struct Bucket {
   // timing (all on the comm stream but ev_ready, recorded on the producer):
   // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
-  bool timed = false;
+  hipEvent_t ev_sync = nullptr;  // untimed ready event (timeline level 0, or not the last bucket at level 1)
+  bool timed = false;            // pk0 / t0 / t1 / u1 recorded (level 2)
+  bool ready_timed = false;      // ev_ready recorded
 };
 
 }  // namespace
@@ -84,6 +86,12 @@ struct gs_bucketer {
   float* dbg = nullptr;        // GSYNC_DEBUG: [3 * n_buckets] Σx after pack, Σx after collective, Σx² after pack
   void* producer = nullptr;
   hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_done_sync = nullptr;  // untimed finalize event (timeline level 0)
+  // timeline level (gs_bucketer_set_timeline): 0 none, 1 the tail only (the
+  // last bucket's ready event + the finalize event, default), 2 every bucket's
+  // queue / pack / collective / unpack.  Each timing event is a packet on the
+  // stream; at level 2 they stretch the exposed chain by ~10 µs apiece.
+  int timeline = 1;
   hipEvent_t ev_comm = nullptr;     // comm stream's earlier buckets, joined before a producer-side tail
   bool done_timed = false;
   bool tail_on_producer = true;     // GSYNC_TAIL_ON_PRODUCER=0 keeps every bucket on the comm stream
@@ -198,7 +206,12 @@ int launch_bucket(gs_bucketer* b, int bi) {
     const bool on_producer = b->tail_on_producer && bi == static_cast<int>(b->buckets.size()) - 1;
     hipStream_t ps = static_cast<hipStream_t>(b->producer);
     hipStream_t cs = on_producer ? ps : comm_stream(b->comm);
-    HIPB_RET(hipEventRecord(bk.ev_ready, ps));
+    // timing events stay out of a hipGraph capture (the timeline then reports -1)
+    const bool capturing = stream_capturing(cs);
+    const bool last = bi == static_cast<int>(b->buckets.size()) - 1;
+    bk.ready_timed = !capturing && (b->timeline >= 2 || (b->timeline == 1 && last));
+    hipEvent_t ready = bk.ready_timed ? bk.ev_ready : bk.ev_sync;
+    HIPB_RET(hipEventRecord(ready, ps));
     if (on_producer) {
       if (bi > 0) {
         HIPB_RET(hipEventRecord(b->ev_comm, comm_stream(b->comm)));
@@ -206,10 +219,9 @@ int launch_bucket(gs_bucketer* b, int bi) {
       }
       b->tail_ran_on_producer = true;
     } else {
-      HIPB_RET(hipStreamWaitEvent(cs, bk.ev_ready, 0));
+      HIPB_RET(hipStreamWaitEvent(cs, ready, 0));
     }
-    // timing events stay out of a hipGraph capture (last_comm_ms then reports -1)
-    const bool timed = !stream_capturing(cs);
+    const bool timed = !capturing && b->timeline >= 2;
     if (timed) HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
     GS_TRY_RET(pack_one(b, bk, cs));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_t0, cs));
@@ -308,7 +320,8 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     if (device_kind == GS_DEV_HIP) {
       if (hipEventCreate(&bk.ev_ready) != hipSuccess || hipEventCreate(&bk.ev_pk0) != hipSuccess ||
           hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess ||
-          hipEventCreate(&bk.ev_u1) != hipSuccess)
+          hipEventCreate(&bk.ev_u1) != hipSuccess ||
+          hipEventCreateWithFlags(&bk.ev_sync, hipEventDisableTiming) != hipSuccess)
         return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
     }
   }
@@ -321,7 +334,8 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
   }
   if (device_kind == GS_DEV_HIP &&
       (hipEventCreateWithFlags(&b->ev_comm, hipEventDisableTiming) != hipSuccess ||
-       hipEventCreate(&b->ev_done) != hipSuccess))
+       hipEventCreate(&b->ev_done) != hipSuccess ||
+       hipEventCreateWithFlags(&b->ev_done_sync, hipEventDisableTiming) != hipSuccess))
     return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
   *out = b;
   return GS_OK;
@@ -333,10 +347,11 @@ int gs_bucketer_destroy(gs_bucketer* b) {
   for (Bucket& bk : b->buckets) {
     gs_plan_destroy(bk.plan);
     gs_plan_destroy(bk.flat);
-    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1})
+    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1, bk.ev_sync})
       if (ev) (void)hipEventDestroy(ev);
   }
   if (b->ev_done) (void)hipEventDestroy(b->ev_done);
+  if (b->ev_done_sync) (void)hipEventDestroy(b->ev_done_sync);
   if (b->ev_comm) (void)hipEventDestroy(b->ev_comm);
   delete b;
   return GS_OK;
@@ -458,17 +473,14 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
   }
   if (b->hip() && b->auto_coll()) {
     hipStream_t ps = static_cast<hipStream_t>(stream);
-    if (b->tail_ran_on_producer && ps == static_cast<hipStream_t>(b->producer)) {
-      // the last bucket ran on the producer after joining the comm stream:
-      // everything is already ordered before this point
-      HIPB_RET(hipEventRecord(b->ev_done, ps));
-      b->done_timed = !stream_capturing(ps);
-    } else {
-      hipStream_t cs = comm_stream(b->comm);
-      HIPB_RET(hipEventRecord(b->ev_done, cs));
-      b->done_timed = !stream_capturing(cs);
-      HIPB_RET(hipStreamWaitEvent(ps, b->ev_done, 0));
-    }
+    const bool on_ps = b->tail_ran_on_producer && ps == static_cast<hipStream_t>(b->producer);
+    hipStream_t ds = on_ps ? ps : comm_stream(b->comm);
+    b->done_timed = b->timeline >= 1 && !stream_capturing(ds);
+    hipEvent_t done = b->done_timed ? b->ev_done : b->ev_done_sync;
+    // the last bucket ran on the producer after joining the comm stream:
+    // everything is already ordered before this point; otherwise join the comm stream
+    if (!on_ps || b->done_timed) HIPB_RET(hipEventRecord(done, ds));
+    if (!on_ps) HIPB_RET(hipStreamWaitEvent(ps, done, 0));
   } else {
     // external collectives (comm hook / process group) are done by now
     for (Bucket& bk : b->buckets) {
@@ -511,16 +523,26 @@ int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out) {
   GS_CHECK_ARG(b && out && bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "bad bucket");
   for (int i = 0; i < 5; ++i) out[i] = -1.f;
   Bucket& bk = b->buckets[bucket];
-  if (!bk.timed || !b->hip() || !b->auto_coll()) return GS_OK;
-  HIPB_RET(hipEventSynchronize(bk.ev_u1));
-  HIPB_RET(hipEventElapsedTime(&out[0], bk.ev_ready, bk.ev_pk0));
-  HIPB_RET(hipEventElapsedTime(&out[1], bk.ev_pk0, bk.ev_t0));
-  HIPB_RET(hipEventElapsedTime(&out[2], bk.ev_t0, bk.ev_t1));
-  HIPB_RET(hipEventElapsedTime(&out[3], bk.ev_t1, bk.ev_u1));
-  if (b->done_timed) {
+  if (!b->hip() || !b->auto_coll()) return GS_OK;
+  if (bk.timed && bk.ready_timed) {
+    HIPB_RET(hipEventSynchronize(bk.ev_u1));
+    HIPB_RET(hipEventElapsedTime(&out[0], bk.ev_ready, bk.ev_pk0));
+    HIPB_RET(hipEventElapsedTime(&out[1], bk.ev_pk0, bk.ev_t0));
+    HIPB_RET(hipEventElapsedTime(&out[2], bk.ev_t0, bk.ev_t1));
+    HIPB_RET(hipEventElapsedTime(&out[3], bk.ev_t1, bk.ev_u1));
+  }
+  if (bk.ready_timed && b->done_timed) {
     HIPB_RET(hipEventSynchronize(b->ev_done));
     HIPB_RET(hipEventElapsedTime(&out[4], bk.ev_ready, b->ev_done));
   }
+  return GS_OK;
+}
+
+int gs_bucketer_set_timeline(gs_bucketer* b, int level) {
+  GS_CHECK_ARG(b != nullptr && level >= 0 && level <= 2, "gs_bucketer_set_timeline: level 0, 1 or 2");
+  std::lock_guard<std::mutex> lk(b->mu);
+  if (b->prepared) return fail(GS_ESTATE, "gs_bucketer_set_timeline inside a backward");
+  b->timeline = level;
   return GS_OK;
 }
 

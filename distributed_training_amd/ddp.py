@@ -392,6 +392,9 @@ class DistributedDataParallel(nn.Module):
         if getattr(self, "_debug_sums", None) is not None:
             self._debug_sums = torch.zeros(3 * len(buckets), dtype=torch.float32, device=self.device)
             L.check(L.lib().gs_bucketer_set_debug(b.handle, self._debug_sums.data_ptr()), "gs_bucketer_set_debug")
+        lvl = getattr(self, "_timeline", None)
+        if lvl is not None:
+            L.check(L.lib().gs_bucketer_set_timeline(b.handle, lvl), "gs_bucketer_set_timeline")
         return b
 
     def _calib_allreduce(self, nbytes: int, iters: int = 4) -> float:
@@ -715,8 +718,19 @@ class DistributedDataParallel(nn.Module):
         """Fuse Σg² of the averaged grads into the unpack (fp32 1-element tensor)."""
         self._sqnorm_target = t
 
+    def set_timeline(self, level: int):
+        """Which HIP timing events the bucket chains record
+        (gs_bucketer_set_timeline): 0 none; 1 (default) the tail total only
+        (:meth:`tail_ms` ``total``); 2 every bucket's queue / pack / collective /
+        unpack (:meth:`bucket_timeline_ms`, :meth:`bucket_comm_ms`).  Each event is
+        a packet on its stream (~10 µs on the exposed tail at level 2), so timed
+        runs stay at level ≤ 1 and read the split from a separate step."""
+        self._timeline = int(level)
+        L.check(L.lib().gs_bucketer_set_timeline(self._bucketer.handle, self._timeline), "gs_bucketer_set_timeline")
+
     def bucket_comm_ms(self):
-        """Per-bucket collective time of the last iteration (HIP events on the comm stream)."""
+        """Per-bucket collective time of the last iteration (HIP events on the
+        comm stream; -1 unless :meth:`set_timeline` is 2)."""
         out = []
         for bi in range(len(self._bucketer.buckets)):
             ms = ctypes.c_float()
@@ -787,7 +801,8 @@ class DistributedDataParallel(nn.Module):
         """The exposed end-of-backward tail of the last iteration: from the
         last bucket's ready event (its last gradient produced) to the
         finalize event every bucket's chain has passed, split into the last
-        bucket's queue / pack / collective / unpack (HIP events)."""
+        bucket's queue / pack / collective / unpack (HIP events; the split is
+        None below timeline level 2)."""
         tl = self.bucket_timeline_ms()
         if not tl or tl[-1]["ready_to_done"] is None:
             return None

@@ -328,6 +328,11 @@ int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
  *   out[4] ready -> every bucket finished (the finalize event): for the last
  *          bucket this is the exposed end-of-backward tail */
 int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out /* [5] */);
+/* which timing events the bucketer records (each is a packet on its stream;
+ * on the exposed chain they cost ~10 µs apiece): 0 none; 1 (default) the last
+ * bucket's ready event + the finalize event — out[4] of the last bucket, the
+ * tail; 2 every bucket's full timeline (and gs_bucketer_last_comm_ms) */
+int gs_bucketer_set_timeline(gs_bucketer* b, int level);
 /* Debug mode (checksum each bucket before and after the
  * collective): with a non-NULL device (host, for host buckets) buffer of
  * 3 * n_buckets floats, every backward writes sums[3b] = Σx of bucket b after

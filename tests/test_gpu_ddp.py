@@ -52,6 +52,7 @@ def test_ddp_ws1_rccl_grads_and_sgd(cuda_device, rccl_pg):
     local = {}
     _snap_hooks(params, local)
     ddp = DistributedDataParallel(model)
+    ddp.set_timeline(2)  # every bucket's HIP events (bucket_comm_ms below)
     assert ddp._comm is not None  # RCCL path, not a fallback
     opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     g = torch.Generator(device=cuda_device).manual_seed(1)
@@ -268,6 +269,8 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
     if mode == "last_bucket_cap":
         kw["last_bucket_cap_mb"] = 0.001
     ddp = DistributedDataParallel(model, **kw)
+    if mode == "last_bucket_cap":
+        ddp.set_timeline(2)  # the tail split below
     if mode == "debug_checksums":
         ddp.enable_bucket_checksums()
     dt = torch.bfloat16 if mode == "bf16_model" else torch.float32
@@ -304,6 +307,13 @@ def test_ddp_ws1_modes(cuda_device, rccl_pg, mode):
         assert len(last) == 1 or sum(params[i].numel() * 4 for i in last) <= 1048
         t = ddp.tail_ms()
         assert t is not None and t["total"] >= t["pack"] >= 0
+        ddp.set_timeline(1)  # default: the tail total only, no split
+        run_one = params[0].grad is None
+        x = torch.rand(8, 3, 32, 32, device=cuda_device)
+        torch.nn.functional.cross_entropy(ddp(x), torch.zeros(8, dtype=torch.long, device=cuda_device)).backward()
+        t = ddp.tail_ms()
+        assert run_one and t is not None and t["total"] >= 0 and t["pack"] is None
+        assert all(ms < 0 for ms in ddp.bucket_comm_ms())
 
 
 def test_communicator_watchdog_and_abort(cuda_device):

@@ -87,6 +87,7 @@ def test_bench_n1_contract(cuda_device):
     assert lines[0]["parity"]["collective"] == "rccl(libgsync)"
     t = lines[0]["grad_sync"]["tail_ms"]  # last bucket ready -> every bucket chain done
     assert t["total"] > 0 and t["pack"] > 0 and t["collective"] >= 0 and t["unpack"] > 0
+    assert t["total_timed_step"] > 0  # the timed steps' own tail (timeline level 1)
     assert len(lines[0]["grad_sync"]["bucket_timeline_ms"]) == lines[0]["grad_sync"]["n_buckets"]
 
 
