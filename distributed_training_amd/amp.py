@@ -66,9 +66,9 @@ class GradScaler:
         if not self._enabled:
             return outputs
         self._lazy_init(outputs.device)
-        # as torch: the fp32 scale multiplies without a cast (an fp16 loss is
-        # promoted to fp32 — the default 2**16 does not fit fp16)
-        return outputs * self._scale.to(device=outputs.device, non_blocking=True)
+        # as torch: the 0-dim fp32 scale multiplies without a cast (an fp16 loss
+        # is promoted to fp32 — the default 2**16 does not fit fp16 — and keeps its shape)
+        return outputs * self._scale.view(()).to(device=outputs.device, non_blocking=True)
 
     def get_scale(self):
         return self._init_scale if self._scale is None else float(self._scale.item())

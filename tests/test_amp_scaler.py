@@ -80,3 +80,20 @@ def test_scaler_cpu_host_backend(kind, poison_at):
 @pytest.mark.parametrize("poison_at", [(0,), (2,), (0, 1, 3)])
 def test_scaler_gpu(cuda_device, kind, poison_at):
     _run(cuda_device, kind, poison_at)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_scale_matches_torch_for_low_precision_loss(dtype):
+    """scale() multiplies by the fp32 scale tensor without casting it
+    (T:amp/grad_scaler.py scale()): an fp16 loss at the default init_scale
+    2**16 (> fp16 max 65504) stays finite and equals torch's bit for bit, in
+    dtype and shape."""
+    loss = torch.tensor(1.2345, dtype=dtype)
+    for shape in ((), (3,)):
+        x = loss.expand(shape).clone() if shape else loss
+        a = GradScaler("cpu").scale(x)
+        b = torch.amp.GradScaler("cpu").scale(x)
+        assert a.dtype == b.dtype and a.shape == b.shape
+        assert torch.equal(a, b)
+        if not shape:  # a scalar loss is promoted to fp32 (a 1-D fp16 tensor is not, in torch too)
+            assert a.dtype == torch.float32 and bool(torch.isfinite(a))
