@@ -466,6 +466,23 @@ def main():
             traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    # the same launches' kernel durations from the committed rocprofv3 kernel trace of
+    # this command (scripts/gpu_round.sh PROFILE=1 -> scripts/trace_roofline.py)
+    trace_check = None
+    trace_json = os.path.join(REPO, "profiles", "trace_roofline.json")
+    if (os.path.exists(trace_json) and zero is None and args.impl == "libgsync" and args.engine == "ddp"
+            and args.model == "resnet50" and args.optimizer == "sgd" and not args.graph):
+        try:
+            with open(trace_json) as f:
+                tr = json.load(f).get("SgdOp")
+            if tr:
+                trace_check = {"kernel_trace_avg_ms": tr["avg_us"] * 1e-3,
+                               "frac_at_trace_duration": bytes_per_param * upd_params / (tr["avg_us"] * 1e-6)
+                               / 1e9 / HBM_PEAK_GBPS,
+                               "source": "profiles/trace_roofline.json: rocprofv3 kernel trace of the timed "
+                                         "launches of this command (the event pair adds the kernel's dispatch)"}
+        except Exception:
+            trace_check = None
     if args.impl == "torch":
         log = ddp._get_ddp_logging_data()
         bucket_bytes = [int(b) for b in str(log.get("rebuilt_bucket_sizes", "")).split(",") if b.strip()]
@@ -562,6 +579,7 @@ def main():
             "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
                        + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")),
             "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
+            **({"rocprof": trace_check} if trace_check else {}),
         },
         "grad_sync": grad_sync,
         "grad_sync_kernels": kernel_rates,

@@ -3,7 +3,8 @@ the reference's GPU path for the same work (torch ops on the same device).
 
 For ResNet-50 / ResNet-152 parameter sets (real per-tensor shapes) it times,
 with HIP events on the stream each kernel is launched on (libgsync rows: the
-plan launch timer, events recorded by the library around each kernel):
+plan launch timer, events recorded by the library around each kernel; every
+row also `batched_*`: the same launches back to back between one event pair):
 
   libgsync                         reference GPU path (torch 2.10 on ROCm)
   pack fp32 (x 1/ws)   8 B/param    per-param  torch.mul(grad, 1/ws, out=bucket_view)  (Reducer mark_variable_ready_dense)
@@ -30,9 +31,13 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 HBM_PEAK = 8000.0
 
 
+_LAST = {}
+
+
 def timeit_plan(plan, fn, iters=20, warmup=3):
     """libgsync launches: the plan launch timer (HIP events recorded by the
     library right around each kernel on its stream)."""
+    _LAST["fn"] = fn
     for _ in range(warmup):
         fn()
     plan.timer_enable(iters)
@@ -43,9 +48,23 @@ def timeit_plan(plan, fn, iters=20, warmup=3):
     return ts[len(ts) // 2], sum(ts) / len(ts)
 
 
+def timeit_batched(fn, iters=20):
+    """`iters` back-to-back launches between ONE pair of HIP events on the
+    current stream (launch gaps included, no per-launch event cost)."""
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(iters):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
 def timeit(fn, iters=20, warmup=3):
     for _ in range(warmup):
         fn()
+    _LAST["fn"] = fn
     s = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
     for a, b in evs:
@@ -83,11 +102,17 @@ def main():
     views16 = [flat16[o:o + torch.Size(s).numel()].view(s) for o, s in zip(offs, shapes)]
     out = []
 
+    last_fn = _LAST
+
     def rec(name, nbytes, ms_med, ms_avg, impl):
         gbs = nbytes / (ms_avg * 1e-3) / 1e9
         row = {"kernel": name, "impl": impl, "model": args.model, "replicas": args.replicas, "params": n,
                "tag": args.tag, "task_units": plan.task_units, "n_tasks": plan.n_tasks,
                "alg_bytes": nbytes, "median_ms": ms_med, "avg_ms": ms_avg, "GBps": gbs, "frac_of_8TBps": gbs / HBM_PEAK}
+        if "fn" in last_fn:  # the same launches, batched between one event pair
+            bms = timeit_batched(last_fn.pop("fn"), args.iters)
+            bgbs = nbytes / (bms * 1e-3) / 1e9
+            row.update({"batched_avg_ms": bms, "batched_GBps": bgbs, "batched_frac_of_8TBps": bgbs / HBM_PEAK})
         out.append(row)
         print(json.dumps(row), flush=True)
 

@@ -36,9 +36,11 @@ fi
 export TMPDIR=/tmp
 if [ "${PROFILE:-0}" == "1" ]; then
   echo "== rocprofv3 kernel trace + stats (bench)"
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o bench -- python3 -u bench.py --gpus 1 --steps 5 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
+  # the timed steps only after the warmup: no kernel-rate / parity launches in the trace
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$TAG -o bench -- python3 -u bench.py --gpus 1 --steps $STEPS --warmup 3 --cpu-baseline 0 --kernel-rates 0 --parity 0 ${BENCH_ARGS:-} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
   find $OUT/prof_$TAG -name "*stats*"
   python3 scripts/overlap.py $(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1) $OUT/overlap_$TAG.json > /dev/null || true
+  python3 scripts/trace_roofline.py $(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1) $STEPS $OUT/trace_roofline_$TAG.json || true
   # keep the summaries (gpurun copies back <= 64 MiB): drop the full traces
   for f in $(find $OUT/prof_$TAG -name "*stats*.csv"); do cp $f $OUT/${TAG}_$(basename $f); done
   rm -rf $OUT/prof_$TAG
