@@ -34,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+HBM_COPY_GBPS = 6290.0  # MI355X_MICROARCH.md's measured float4 copy ceiling (report both)
 XGMI_LINK_GBPS = 153.0  # per point-to-point link; bus roofline (n-1) x 153
 
 
@@ -572,6 +573,8 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+            "copy_ceiling": HBM_COPY_GBPS,
+            "frac_of_copy_ceiling": achieved / HBM_COPY_GBPS if achieved else None,
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
             "avg_launch_ms": opt_ms_avg,
