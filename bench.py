@@ -85,6 +85,9 @@ def parse():
                     help="after the timed region: one self-checked step (distributed_training_amd.parity)")
     ap.add_argument("--kernel-rates", type=int, default=1,
                     help="after the timed region: every grad-sync kernel alone on this model's params (rank 0)")
+    ap.add_argument("--optimizer-overlap", type=int, default=0,
+                    help="1: DDP._register_fused_optim — each bucket's fused update runs behind its unpack "
+                         "under backward (torch's overlapped-optimizer API); no optimizer.step() after backward")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -210,6 +213,34 @@ def grad_sync_kernel_rates(params, dev, iters=20):
                       f"{iters} launches", "min_frac": min(r["frac"] for r in rows.values())}
 
 
+class _OverlappedStep:
+    """The bench's optimizer handle under --optimizer-overlap: the update already
+    ran per bucket inside backward, so step() is empty; kernel_ms() is the sum
+    over the buckets' launches of each step (one whole-model update per step)."""
+
+    def __init__(self, ddp):
+        self.ddp = ddp
+        self.main = ddp._overlapped_optimizer
+
+    def _opts(self):
+        return [o for o in self.ddp._overlap["per_bucket"].values() if o]
+
+    def step(self):
+        pass
+
+    def zero_grad(self, set_to_none=True):
+        self.main.zero_grad(set_to_none=set_to_none)
+
+    def enable_kernel_timer(self, n):
+        for o in self._opts():
+            o.enable_kernel_timer(n)
+
+    def kernel_ms(self):
+        per = [o.kernel_ms() for o in self._opts()]
+        n = min((len(x) for x in per), default=0)
+        return [sum(x[k] for x in per) for k in range(n)]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -261,7 +292,16 @@ def main():
         ddp = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
                                         gradient_as_bucket_view=args.grad_as_bucket_view,
                                         bucket_policy=args.bucket_policy, last_bucket_cap_mb=args.last_bucket_cap_mb)
-        if args.optimizer == "sgd":
+        if args.optimizer_overlap:
+            if args.graph:
+                raise SystemExit("--optimizer-overlap: eager only")
+            if args.optimizer == "sgd":
+                ddp._register_fused_optim(torch.optim.SGD, lr=0.1, momentum=0.9, weight_decay=1e-4)
+            else:
+                ddp._register_fused_optim(torch.optim.Adam, lr=1e-3 * world)
+            opt = _OverlappedStep(ddp)
+            bytes_per_param = 20 if args.optimizer == "sgd" else 28
+        elif args.optimizer == "sgd":
             opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4,
                              capturable=bool(args.graph))
             bytes_per_param = 20  # p r/w, g r, buf r/w (fp32)
@@ -556,6 +596,7 @@ def main():
             "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
             "impl": args.impl,
             "hipgraph": bool(args.graph),
+            "optimizer_overlap": bool(args.optimizer_overlap),
             **({"rehearsal": "gloo, ranks sharing GPUs: control flow only, not a measurement"}
                if args.pg_backend == "gloo" else {}),
             "params": n_params,
@@ -580,7 +621,9 @@ def main():
             "avg_launch_ms": opt_ms_avg,
             "launches": len(opt_ms),
             "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
-                       + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")),
+                       + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
+                       + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
+                          if args.optimizer_overlap else "")),
             "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
             **({"rocprof": trace_check} if trace_check else {}),
         },

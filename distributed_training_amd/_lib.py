@@ -140,6 +140,7 @@ SIGNATURES = {
     "gs_bucketer_last_comm_ms": (_c_int, [_vp, _c_int, _p_f]),
     "gs_bucketer_last_timing": (_c_int, [_vp, _c_int, _p_f]),
     "gs_bucketer_set_timeline": (_c_int, [_vp, _c_int]),
+    "gs_bucketer_bucket_stream": (_c_int, [_vp, _c_int, ctypes.POINTER(_vp)]),
 }
 
 

@@ -54,6 +54,7 @@ struct Bucket {
   int pending = 0;
   bool launched = false;
   bool unpacked = false;
+  void* stream = nullptr;       // the stream this iteration's chain ran on (gs_bucketer_bucket_stream)
   // timing (all on the comm stream but ev_ready, recorded on the producer):
   // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
@@ -231,6 +232,7 @@ int launch_bucket(gs_bucketer* b, int bi) {
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
     if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
     if (timed) HIPB_RET(hipEventRecord(bk.ev_u1, cs));
+    bk.stream = cs;
   } else {
     GS_TRY_RET(pack_one(b, bk, b->producer));
   }
@@ -535,6 +537,15 @@ int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out) {
     HIPB_RET(hipEventSynchronize(b->ev_done));
     HIPB_RET(hipEventElapsedTime(&out[4], bk.ev_ready, b->ev_done));
   }
+  return GS_OK;
+}
+
+int gs_bucketer_bucket_stream(gs_bucketer* b, int bucket, void** stream) {
+  GS_CHECK_ARG(b != nullptr && stream != nullptr, "gs_bucketer_bucket_stream: NULL argument");
+  std::lock_guard<std::mutex> lk(b->mu);
+  GS_CHECK_ARG(bucket >= 0 && bucket < static_cast<int>(b->buckets.size()), "gs_bucketer_bucket_stream: bad bucket");
+  const Bucket& bk = b->buckets[bucket];
+  *stream = (b->hip() && b->auto_coll() && bk.launched) ? bk.stream : nullptr;
   return GS_OK;
 }
 

@@ -367,6 +367,7 @@ class DistributedDataParallel(nn.Module):
         self._pending: dict[int, Any] = {}
         self._num_iterations = 0
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
+        self._overlap: dict | None = None  # _register_fused_optim state
         self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                               for i, p in enumerate(self._params)]
 
@@ -395,6 +396,8 @@ class DistributedDataParallel(nn.Module):
         lvl = getattr(self, "_timeline", None)
         if lvl is not None:
             L.check(L.lib().gs_bucketer_set_timeline(b.handle, lvl), "gs_bucketer_set_timeline")
+        if getattr(self, "_overlap", None) is not None:
+            self._overlap["per_bucket"] = {}  # bucket membership changed
         return b
 
     def _calib_allreduce(self, nbytes: int, iters: int = 4) -> float:
@@ -602,8 +605,12 @@ class DistributedDataParallel(nn.Module):
             b = self._bucketer
             L.check(L.lib().gs_bucketer_mark_ready(b.handle, idx, g.data_ptr(), self._stream, b._ready,
                                                    ctypes.byref(b._n_ready)), "gs_bucketer_mark_ready")
-            if b._n_ready.value and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
-                self._launch_external([b._ready[k] for k in range(b._n_ready.value)])
+            if b._n_ready.value:
+                ready = [b._ready[k] for k in range(b._n_ready.value)]
+                if not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+                    self._launch_external(ready)
+                elif self._overlap is not None:
+                    self._overlap_step(ready)
 
         return hook
 
@@ -628,8 +635,12 @@ class DistributedDataParallel(nn.Module):
         if self.find_unused_parameters:
             L.check(L.lib().gs_bucketer_mark_unused(b.handle, self._stream, b._ready, ctypes.byref(b._n_ready)),
                     "gs_bucketer_mark_unused")
-            if b._n_ready.value and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
-                self._launch_external([b._ready[k] for k in range(b._n_ready.value)])
+            if b._n_ready.value:
+                ready = [b._ready[k] for k in range(b._n_ready.value)]
+                if not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+                    self._launch_external(ready)
+                elif self._overlap is not None:
+                    self._overlap_step(ready)
         for bi in sorted(self._pending):
             kind, obj = self._pending[bi]
             if kind == "work":
@@ -642,6 +653,10 @@ class DistributedDataParallel(nn.Module):
                     b.buffers[bi].copy_(res.reshape(-1)[: b.buffers[bi].numel()])
         self._pending = {}
         L.check(L.lib().gs_bucketer_finalize(b.handle, self._stream), "gs_bucketer_finalize")
+        if self._overlap is not None and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+            # external collectives (gloo, host buckets): the grads exist once the
+            # bucketer has unpacked them at finalize — step every bucket then
+            self._overlap_step(range(len(b.buckets)))
         self._found_inf_valid = self._found_inf_target is not None
         if self.gradient_as_bucket_view:
             for i, p in enumerate(self._params):
@@ -692,11 +707,78 @@ class DistributedDataParallel(nn.Module):
             pos += c
         return out
 
+    def _overlap_step(self, bucket_ids):
+        """The overlapped optimizer's update of buckets `bucket_ids`: one fused
+        kernel per bucket on the stream its chain ran on, behind its unpack."""
+        ov = self._overlap
+        main = ov["opt"]
+        hyper = {k: v for k, v in main.param_groups[0].items() if k != "params"}
+        for bi in bucket_ids:
+            bo = ov["per_bucket"].get(bi)
+            if bo is None:
+                members = [self._params[i] for i in self._bucketer.buckets[bi] if id(self._params[i]) in ov["ids"]]
+                bo = ov["cls"](members, *ov["args"], **ov["kwargs"]) if members else False
+                if bo:
+                    bo.state = main.state  # one optimizer state across the buckets (state_dict: ov["opt"])
+                ov["per_bucket"][bi] = bo
+            if not bo:
+                continue
+            bo.param_groups[0].update(hyper)  # lr schedules act on the main optimizer's group
+            ptr = ctypes.c_void_p()
+            L.check(L.lib().gs_bucketer_bucket_stream(self._bucketer.handle, bi, ctypes.byref(ptr)),
+                    "gs_bucketer_bucket_stream")
+            if ptr.value:
+                st = ov["streams"].get(ptr.value)
+                if st is None:
+                    st = ov["streams"][ptr.value] = torch.cuda.ExternalStream(ptr.value, device=self.device)
+                with torch.cuda.stream(st):
+                    bo.step()
+            else:
+                bo.step()
+
     # ------------------------------------------------------------------ API
+    def _register_fused_optim(self, optim: type, *args, optim_params=None, **kwargs):
+        """Overlapped optimizer (T:nn/parallel/distributed.py ``_register_fused_optim``,
+        T:distributed/algorithms/_optimizer_overlap/optimizer_overlap.py and
+        ddp_comm_hooks/optimizer_overlap_hooks.py ``_hook_then_optimizer``):
+        each bucket's parameters are updated as soon as its averaged grads
+        exist, so the update runs under the rest of backward instead of after it.
+        torch chains a functional per-parameter ``step_param`` on the bucket's
+        future; here ONE fused SGD / Adam(W) kernel per bucket is enqueued on the
+        stream the bucket's pack -> collective -> unpack chain ran on
+        (``gs_bucketer_bucket_stream``), right behind its unpack.  As in torch:
+        call once, the caller no longer calls ``optimizer.step()``, no comm hook,
+        and ``no_sync`` accumulation updates at the next synchronising backward.
+        ``optim``: torch.optim.SGD / Adam / AdamW or FusedSGD / FusedAdam(W)
+        (same arguments); the optimizer holding the state is
+        ``ddp._overlapped_optimizer`` (state_dict, lr schedules)."""
+        import inspect
+
+        from .optim import FusedAdam, FusedAdamW, FusedSGD
+
+        if self._overlap is not None:
+            raise RuntimeError("_register_fused_optim should only be called once on a DDP instance")
+        if self._comm_hook is not None:
+            raise RuntimeError("_register_fused_optim and register_comm_hook do not compose (as in torch)")
+        table = {torch.optim.SGD: FusedSGD, torch.optim.Adam: FusedAdam, torch.optim.AdamW: FusedAdamW,
+                 FusedSGD: FusedSGD, FusedAdam: FusedAdam, FusedAdamW: FusedAdamW}
+        cls = next((table[c] for c in inspect.getmro(optim) if c in table), None)
+        if cls is None:
+            raise RuntimeError(f"{optim} does not support overlapped DDP (SGD, Adam, AdamW)")
+        if kwargs.get("max_grad_norm"):
+            raise RuntimeError("overlapped optimizer: a global-norm clip needs every bucket before any update")
+        params = list(optim_params) if optim_params is not None else list(self._params)
+        opt = cls(params, *args, **kwargs)
+        self._overlap = {"cls": cls, "args": args, "kwargs": kwargs, "opt": opt, "ids": {id(p) for p in params},
+                         "per_bucket": {}, "streams": {}}
+        self._overlapped_optimizer = opt
+
     def register_comm_hook(self, state: object, hook: Callable):
         """hook(state, GradBucket) -> torch.futures.Future[Tensor] (T:nn/parallel/distributed.py:1953)."""
         if self._comm_hook is not None:
             raise RuntimeError("register_comm_hook or register_builtin_comm_hook can only be called once.")
+        if self._overlap is not None:
+            raise RuntimeError("register_comm_hook and _register_fused_optim do not compose (as in torch)")
         if not callable(hook):
             raise TypeError("Communication hook must be callable.")
         self._comm_hook = (state, hook)

@@ -333,6 +333,14 @@ int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out /* [5] */);
  * bucket's ready event + the finalize event — out[4] of the last bucket, the
  * tail; 2 every bucket's full timeline (and gs_bucketer_last_comm_ms) */
 int gs_bucketer_set_timeline(gs_bucketer* b, int level);
+/* the HIP stream bucket `bucket`'s chain (pack -> collective -> unpack) was
+ * enqueued on in this backward (the comm stream, or the producer stream for the
+ * last bucket); NULL before its launch, on the host and with external
+ * collectives.  Work enqueued there after the chain sees the averaged grads —
+ * the overlapped optimizer (DDP._register_fused_optim) steps each bucket so.
+ * replaces: the Future of run_comm_hook that _hook_then_optimizer chains on
+ *           (T:distributed/algorithms/ddp_comm_hooks/optimizer_overlap_hooks.py) */
+int gs_bucketer_bucket_stream(gs_bucketer* b, int bucket, void** stream);
 /* Debug mode (checksum each bucket before and after the
  * collective): with a non-NULL device (host, for host buckets) buffer of
  * 3 * n_buckets floats, every backward writes sums[3b] = Σx of bucket b after

@@ -1,0 +1,102 @@
+"""The overlapped optimizer (DDP._register_fused_optim, T:nn/parallel/distributed.py
+``_register_fused_optim``; torch/distributed/algorithms/_optimizer_overlap) on
+CPU / gloo, world size 2:
+
+* libgsync DDP + ``_register_fused_optim(SGD | Adam)`` == libgsync DDP +
+  an explicit fused ``optimizer.step()`` after backward, bit for bit (the same
+  elementwise update, launched per bucket instead of once);
+* == torch's DDP + its own ``_register_fused_optim`` (functional per-parameter
+  ``step_param``) within SURVEY.md §8c's tolerances (SGD rtol 1e-6 / atol 1e-7,
+  fma placement; Adam atol lr·1e-3);
+* the API contract: one registration, no comm hook beside it, lr changes on
+  ``ddp._overlapped_optimizer`` reach the per-bucket updates, ``no_sync``
+  accumulates and the next synchronising backward updates once."""
+import pytest
+import torch
+import torch.nn as nn
+
+from tests.test_ddp_cpu import _micro, _run
+
+STEPS = 3
+
+
+def _batches(rank, n):
+    g = torch.Generator().manual_seed(1234 + rank)
+    return [(torch.rand(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)) for _ in range(n)]
+
+
+def _train(rank, kind, impl, overlap):
+    import distributed_training_amd as D
+
+    torch.manual_seed(0)
+    model = _micro()
+    opt_cls = {"sgd": torch.optim.SGD, "adam": torch.optim.Adam}[kind]
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-4) if kind == "sgd" else dict(lr=1e-3)
+    if impl == "torch":
+        ddp = torch.nn.parallel.DistributedDataParallel(model)
+    else:
+        ddp = D.DistributedDataParallel(model)
+    opt = None
+    if overlap:
+        ddp._register_fused_optim(opt_cls, **kw)
+    else:
+        opt = (D.FusedSGD if kind == "sgd" else D.FusedAdam)(ddp.parameters(), **kw)
+    for x, y in _batches(rank, STEPS):
+        nn.functional.cross_entropy(ddp(x), y).backward()
+        if opt is not None:
+            opt.step()
+        for p in model.parameters():
+            p.grad = None
+    return [p.detach().clone() for p in model.parameters()], ddp
+
+
+def _compare(rank, ws, kind):
+    ref, _ = _train(rank, kind, "libgsync", overlap=False)
+    got, ddp = _train(rank, kind, "libgsync", overlap=True)
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert torch.equal(a, b), f"{kind} param {i}: overlapped != explicit step"
+    tor, _ = _train(rank, kind, "torch", overlap=True)
+    tol = dict(rtol=1e-6, atol=1e-7) if kind == "sgd" else dict(rtol=0, atol=1e-3 * 1e-3)
+    for i, (a, b) in enumerate(zip(tor, got)):
+        torch.testing.assert_close(b, a, **tol, msg=lambda m: f"{kind} param {i} vs torch overlap: {m}")
+    st = ddp._overlapped_optimizer.state
+    assert len(st) == len(got)  # one state for every parameter, held by the main optimizer
+    if kind == "adam":
+        assert all(float(s["step"]) == STEPS for s in st.values())
+
+
+def _contract(rank, ws):
+    import distributed_training_amd as D
+
+    torch.manual_seed(0)
+    model = _micro()
+    ddp = D.DistributedDataParallel(model)
+    ddp._register_fused_optim(torch.optim.SGD, lr=0.0)
+    with pytest.raises(RuntimeError):
+        ddp._register_fused_optim(torch.optim.SGD, lr=0.1)
+    with pytest.raises(RuntimeError):
+        ddp.register_comm_hook(None, lambda s, b: None)
+    (x, y), (x2, y2) = _batches(rank, 2)
+    w0 = [p.detach().clone() for p in model.parameters()]
+    nn.functional.cross_entropy(ddp(x), y).backward()  # lr 0: nothing moves
+    assert all(torch.equal(a, p) for a, p in zip(w0, model.parameters()))
+    for p in model.parameters():
+        p.grad = None
+    ddp._overlapped_optimizer.param_groups[0]["lr"] = 0.1  # a schedule acts on the main optimizer
+    with ddp.no_sync():
+        nn.functional.cross_entropy(ddp(x), y).backward()
+    assert all(torch.equal(a, p) for a, p in zip(w0, model.parameters()))  # no update without sync
+    nn.functional.cross_entropy(ddp(x2), y2).backward()
+    moved = sum(not torch.equal(a, p) for a, p in zip(w0, model.parameters()))
+    assert moved == len(w0)
+    with pytest.raises(RuntimeError):
+        D.DistributedDataParallel(_micro())._register_fused_optim(torch.optim.RMSprop, lr=0.1)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_overlapped_optimizer_matches_explicit_step_and_torch(kind):
+    _run(_compare, 2, kind)
+
+
+def test_overlapped_optimizer_contract():
+    _run(_contract, 2)

@@ -349,3 +349,67 @@ def test_communicator_watchdog_and_abort(cuda_device):
     with pytest.raises(L.GsyncError, match="aborted"):
         c.check()
     c.close()
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adamw"])
+def test_overlapped_optimizer_ws1_rccl(cuda_device, rccl_pg, kind):
+    """DDP._register_fused_optim on the AUTO-collective path: each bucket's
+    fused update is enqueued behind its unpack on the stream its chain ran on
+    (the comm stream; the producer stream for the last bucket), under the rest
+    of backward.  Every iteration (bucket rebuild included), against the oracle
+    on the same run's data (MIOpen's backward is not bitwise run-to-run, so two
+    runs are not compared): the grads the hooks saw == the averaged grads
+    (ws=1) and the weights after backward == oracle SGD / AdamW of the weights
+    before it with those grads, bit for bit — no update read a partial unpack
+    or a weight the backward still used."""
+    import ctypes
+
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.manual_seed(0)
+    model = micro_resnet().to(cuda_device).to(memory_format=torch.channels_last)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)  # before DDP's hooks: the local grad, ahead of the chain
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.02)  # several buckets after the rebuild
+    if kind == "sgd":
+        ddp._register_fused_optim(torch.optim.SGD, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    else:
+        ddp._register_fused_optim(torch.optim.AdamW, lr=1e-3, weight_decay=1e-2)
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    state = {}
+    for it in range(4):
+        x = torch.rand(8, 3, 32, 32, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (8,), device=cuda_device, generator=g)
+        out = ddp(x)  # the forward reads the weights: snapshot them after it (same stream)
+        before = [to_np(p).reshape(-1).copy() for p in params]
+        torch.nn.functional.cross_entropy(out, y).backward()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            gl = to_np(local[i]).reshape(-1)
+            assert np.array_equal(to_np(p.grad).reshape(-1), gl), f"iter {it} param {i} grad"
+            if kind == "sgd":
+                st = state.get(i)
+                w, buf = O.sgd(before[i], gl, st, 0.05, 0.9, 0.0, 1e-4, False, False, st is None)
+                state[i] = buf
+            else:
+                m, v = state.get(i, (np.zeros_like(gl), np.zeros_like(gl)))
+                w, m, v = O.adam(before[i], gl, m, v, it + 1, 1e-3, weight_decay=1e-2, adamw=True)
+                state[i] = (m, v)
+            assert np.array_equal(to_np(p).reshape(-1), w), f"{kind} iter {it} param {i} weights"
+        for p in params:
+            p.grad = None
+    nb = len(ddp.bucket_indices())
+    assert nb > 2 and ddp._get_ddp_logging_data()["has_rebuilt_buckets"] == 1
+    comm = ctypes.c_void_p()
+    L.check(L.lib().gs_comm_stream(ddp._comm.handle, ctypes.byref(comm)), "gs_comm_stream")
+    streams = []
+    for bi in range(nb):
+        s = ctypes.c_void_p()
+        L.check(L.lib().gs_bucketer_bucket_stream(ddp._bucketer.handle, bi, ctypes.byref(s)), "stream")
+        streams.append(s.value)
+    assert all(s == comm.value for s in streams[:-1])  # updates under backward, on the comm stream
+    # the tail runs on the producer stream (here the default stream, handle 0)
+    assert (streams[-1] or 0) == (torch.cuda.current_stream(cuda_device).cuda_stream or 0)
