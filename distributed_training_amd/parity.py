@@ -204,7 +204,10 @@ def zero_parity_step(zero, run_forward_backward, k: int = 6) -> dict:
     for i in idx:
         b, off = zero.loc[i]
         p = params[i]
-        avg_parts.append(fulls[b][off:off + p.numel()].float())
+        # the bucket holds each grad in its parameter's memory order (channels_last
+        # convs included): view the slot with the parameter's strides, as the
+        # engine's own param views are built (zero._build_flat_state)
+        avg_parts.append(fulls[b].as_strided(p.size(), p.stride(), off).reshape(-1).float())
         loc_parts.append(cap[i].reshape(-1).float())
     gathered = coll.all_gather(torch.cat(loc_parts))
     grads = compare_average(torch.cat(avg_parts), gathered, coll.world, zero.dtype)

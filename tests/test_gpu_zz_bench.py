@@ -116,3 +116,29 @@ def test_bench_colossal_engine(cuda_device):
     assert d["roofline"]["algorithmic_bytes_per_launch"] == 28 * d["config"]["params"]
     assert d["roofline"]["launches"] == 3 and d["roofline"]["achieved"] > 0
     assert d["parity"]["ok"] is True and d["parity"]["averaged_grads"]["bitwise_equal"] is True
+
+
+@pytest.mark.parametrize("engine", ["ddp", "zero2"])
+def test_bench_collective_bench_leg(cuda_device, engine):
+    """The standalone collective leg the driver's N>1 runs take by default
+    (`--collective-bench -1` = on when N>1), forced on at N=1 over libgsync's
+    RCCL communicator: every bucket's all-reduce (DDP) or reduce-scatter +
+    all-gather (ZeRO-2), the whole-gradient message and the 1-64 MiB curve;
+    DDP with the overlapped optimizer, the parity step after it."""
+    extra = ["--collective-bench", "1", "--kernel-rates", "0"]
+    extra += ["--optimizer-overlap", "1"] if engine == "ddp" else ["--engine", "zero2"]
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL + extra, cwd=REPO, env=_env(),
+                       capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _json_lines(p.stdout)[0]
+    sb = d["grad_sync"]["standalone"]
+    ops = {r["op"] for r in sb["per_op"]}
+    if engine == "ddp":
+        assert {"all_reduce", "all_reduce_whole_grad", "all_reduce_1MiB", "all_reduce_64MiB"} <= ops
+        assert d["config"]["optimizer_overlap"] is True
+        assert d["grad_sync"]["tail_ms"]["total_timed_step"] > 0
+    else:
+        assert {"reduce_scatter", "all_gather"} <= ops
+    assert all(r["median_ms"] > 0 for r in sb["per_op"])
+    assert sb["xgmi_peak_GBps"] == 0 and sb["frac"] is None  # one rank: no link in use
+    assert d["parity"]["ok"] is True and d["parity"]["collective"] == "rccl(libgsync)", d["parity"]

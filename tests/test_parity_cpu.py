@@ -73,15 +73,17 @@ def test_ddp_parity_step_catches_a_broken_sync():
     _run(_ddp_parity, 2, True)
 
 
-def _zero_parity(rank, ws):
+def _zero_parity(rank, ws, channels_last=False):
     from distributed_training_amd import parity as PC
     from distributed_training_amd.zero import ZeroDataParallel
 
     torch.manual_seed(0)
     model = _micro()
+    mf = torch.channels_last if channels_last else torch.contiguous_format
+    model = model.to(memory_format=mf)  # bench.py's layout: the bucket holds grads in memory order
     zero = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=1e-3, weight_decay=3e-7, gradient_clipping=1.0)
     g = torch.Generator().manual_seed(1234 + rank)
-    x = torch.rand(4, 3, 32, 32, generator=g)
+    x = torch.rand(4, 3, 32, 32, generator=g).to(memory_format=mf)
     y = torch.randint(0, 10, (4,), generator=g)
 
     def fb():
@@ -96,9 +98,10 @@ def _zero_parity(rank, ws):
         assert res["averaged_grads"]["bitwise_equal"], res
 
 
+@pytest.mark.parametrize("channels_last", [False, True])
 @pytest.mark.parametrize("ws", [2, 3])
-def test_zero_parity_step_passes(ws):
-    _run(_zero_parity, ws)
+def test_zero_parity_step_passes(ws, channels_last):
+    _run(_zero_parity, ws, channels_last)
 
 
 def test_split_last_bucket():
