@@ -330,6 +330,20 @@ int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, 
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   hipStream_t s = pick(c, stream);
+  if (c->world == 1) {
+    // One rank: the gather is a copy.  ROCm 7.2's RCCL (2.27.7) runs its
+    // single-rank out-of-place all-gather of >= ~4 MB without waiting for the
+    // work already queued on `s` (scripts/diag_allgather.py: the output's
+    // preceding fill lands after the copy), so the copy is enqueued here, in
+    // stream order.  Every other collective, and every world > 1, goes to RCCL.
+    if (send != recv && send_count > 0) {
+      GS_CHECK_ARG(!c->aborted.load(), "gs_all_gather: communicator aborted");
+      const size_t bytes = static_cast<size_t>(send_count) * dtype_size(dtype);
+      if (hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return fail(GS_EHIP, "gs_all_gather: single-rank copy failed");
+    }
+    return GS_OK;
+  }
   return comm_enqueue(c, s, [&] { return ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, s); },
                       "ncclAllGather");
 }

@@ -51,6 +51,8 @@ class _Coll:
         t = t.contiguous().reshape(-1)
         if self.comm is not None:
             out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+            # the checker does not lean on the collective's stream ordering
+            torch.cuda.current_stream(t.device).synchronize()
             self.comm.all_gather(t, out, stream=L.stream_ptr(t.device))
             torch.cuda.current_stream(t.device).synchronize()
             return out.view(self.world, -1)
