@@ -90,9 +90,11 @@ int to_nccl_op(int op, ncclRedOp_t* out) {
   }
 }
 
-hipStream_t pick(gs_comm* c, void* stream) {
-  return stream ? static_cast<hipStream_t>(stream) : c->stream;
-}
+// NULL is HIP's legacy default stream, as everywhere in the ABI: torch's
+// default stream has handle 0, and mapping it to the (non-blocking) comm
+// stream would drop the order with the work the caller queued before the
+// collective (a pack, a fill).  gs_comm_stream() hands out the comm stream.
+hipStream_t pick(gs_comm*, void* stream) { return static_cast<hipStream_t>(stream); }
 
 // caller holds c->mu
 void abort_locked(gs_comm* c, const std::string& why) {
@@ -330,20 +332,6 @@ int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, 
   ncclDataType_t dt;
   GS_TRY_RET(to_nccl_dtype(dtype, &dt));
   hipStream_t s = pick(c, stream);
-  if (c->world == 1) {
-    // One rank: the gather is a copy.  ROCm 7.2's RCCL (2.27.7) runs its
-    // single-rank out-of-place all-gather of >= ~4 MB without waiting for the
-    // work already queued on `s` (scripts/diag_allgather.py: the output's
-    // preceding fill lands after the copy), so the copy is enqueued here, in
-    // stream order.  Every other collective, and every world > 1, goes to RCCL.
-    if (send != recv && send_count > 0) {
-      GS_CHECK_ARG(!c->aborted.load(), "gs_all_gather: communicator aborted");
-      const size_t bytes = static_cast<size_t>(send_count) * dtype_size(dtype);
-      if (hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
-        return fail(GS_EHIP, "gs_all_gather: single-rank copy failed");
-    }
-    return GS_OK;
-  }
   return comm_enqueue(c, s, [&] { return ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, s); },
                       "ncclAllGather");
 }

@@ -120,7 +120,9 @@ int gs_comm_stream(gs_comm* c, void** stream_out);
 /* make `waiter` wait for all work queued so far on `signaler` (event edge) */
 int gs_stream_wait(void* waiter, void* signaler);
 
-/* collectives; stream NULL = the comm's own stream.  count in elements. */
+/* collectives on `stream` (NULL = the legacy default stream, like every
+ * stream argument; gs_comm_stream() gives the communicator's own stream).
+ * count in elements. */
 int gs_allreduce(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
                  void* stream);
 int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,

@@ -1,6 +1,8 @@
-"""Diagnostic: libgsync's RCCL (ROCm 7.2 librccl) single-rank collectives vs
-stream order — is prior work on the stream (the output's fill) ordered before
-the collective's copy?  Prints matches per case."""
+"""Diagnostic: libgsync's communicator collectives vs stream order — is the
+work queued before a collective on the caller's stream (the output's fill)
+ordered before it?  `side` runs on a created stream instead of the default
+one (handle 0, which the ABI once mistook for "the comm stream").  Prints
+per case whether the output is exact."""
 import os
 import sys
 
@@ -14,7 +16,11 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 from distributed_training_amd.comm import get_communicator  # noqa: E402
 
 c = get_communicator(None, torch.device("cuda", 0))
+side = torch.cuda.Stream()
+if len(sys.argv) > 1 and sys.argv[1] == "side":  # a created (non-null) stream instead of the default one
+    torch.cuda.set_stream(side)
 cur = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+print("stream handle", cur(), flush=True)
 for n in (1 << 20, 1 << 22, 1 << 24):
     for dt in (torch.float32, torch.int32, torch.bfloat16):
         x = (torch.arange(n, device="cuda") % 1000 + 1).to(dt)

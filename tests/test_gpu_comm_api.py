@@ -5,10 +5,10 @@ all-gather, the parity step's all-gather and MIN/MAX checksum all-reduces,
 bench.py's standalone collective leg — on every dtype they carry, on an
 explicit stream and on the comm stream.  At world 1 each is the identity, so
 a wrong count unit, dtype or op mapping shows as a changed or untouched
-output — and so did ROCm 7.2 RCCL's single-rank out-of-place all-gather of
->= 4 Mi elements, which ran ahead of the output's fill queued before it on the
-same stream (scripts/diag_allgather.py); gs_all_gather copies in stream order
-at world 1.  Also DDP's N>1-only helpers (_broadcast_tensors / _sync_buffers),
+output.  The calls go on torch's DEFAULT stream (handle 0): the entry points
+once read a NULL stream as the communicator's own (non-blocking) stream, so
+the collective ran unordered with the fill queued before it — visible at
+4 Mi elements.  Also DDP's N>1-only helpers (_broadcast_tensors / _sync_buffers),
 run through the communicator by faking the world size on the root rank."""
 import pytest
 import torch
@@ -40,7 +40,7 @@ def _data(dt, n, dev):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.float64])
-@pytest.mark.parametrize("n", [1, 1000, 1 << 20, 1 << 22])  # >= 4 Mi: RCCL's single-rank all-gather race
+@pytest.mark.parametrize("n", [1, 1000, 1 << 20, 1 << 22])  # 4 Mi: large enough to lose a stream race
 def test_collectives_identity_at_world_1(comm, cuda_device, dt, n):
     x = _data(dt, n, cuda_device)
     cur = torch.cuda.current_stream(cuda_device).cuda_stream
