@@ -718,12 +718,14 @@ class DistributedDataParallel(nn.Module):
             if bo is None:
                 members = [self._params[i] for i in self._bucketer.buckets[bi] if id(self._params[i]) in ov["ids"]]
                 bo = ov["cls"](members, *ov["args"], **ov["kwargs"]) if members else False
-                if bo:
-                    bo.state = main.state  # one optimizer state across the buckets (state_dict: ov["opt"])
                 ov["per_bucket"][bi] = bo
             if not bo:
                 continue
-            bo.param_groups[0].update(hyper)  # lr schedules act on the main optimizer's group
+            # one optimizer state across the buckets, held by the main optimizer (its
+            # state_dict / load_state_dict, which may replace the dict); lr schedules
+            # act on the main optimizer's group
+            bo.state = main.state
+            bo.param_groups[0].update(hyper)
             ptr = ctypes.c_void_p()
             L.check(L.lib().gs_bucketer_bucket_stream(self._bucketer.handle, bi, ctypes.byref(ptr)),
                     "gs_bucketer_bucket_stream")

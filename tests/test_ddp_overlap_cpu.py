@@ -89,6 +89,16 @@ def _contract(rank, ws):
     nn.functional.cross_entropy(ddp(x2), y2).backward()
     moved = sum(not torch.equal(a, p) for a, p in zip(w0, model.parameters()))
     assert moved == len(w0)
+    # a checkpoint round trip through the main optimizer reaches the per-bucket updates
+    sd = ddp._overlapped_optimizer.state_dict()
+    ddp._overlapped_optimizer.load_state_dict(sd)
+    w1 = [p.detach().clone() for p in model.parameters()]
+    for p in model.parameters():
+        p.grad = None
+    nn.functional.cross_entropy(ddp(x), y).backward()
+    per_bucket = [o for o in ddp._overlap["per_bucket"].values() if o]
+    assert per_bucket and all(o.state is ddp._overlapped_optimizer.state for o in per_bucket)
+    assert all(not torch.equal(a, p) for a, p in zip(w1, model.parameters()))
     with pytest.raises(RuntimeError):
         D.DistributedDataParallel(_micro())._register_fused_optim(torch.optim.RMSprop, lr=0.1)
 

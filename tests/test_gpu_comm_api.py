@@ -88,3 +88,20 @@ def test_ddp_broadcast_helpers_through_the_communicator(comm, cuda_device):
     after = list(model.parameters()) + list(model.buffers())
     for i, (a, b) in enumerate(zip(before, after)):
         assert a.dtype == b.dtype and torch.equal(a, b.detach()), i
+
+
+def test_xgmi_calibration_through_the_communicator(comm, cuda_device):
+    """bucket_policy="xgmi" (N>1 only) times all-reduces on the DDP's own
+    communicator and fits the caps: the same code at world 1 (the fit fed a
+    pretend world of 8) runs RCCL on the default stream and returns caps inside
+    their clamps."""
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd.ddp import xgmi_bucket_caps
+    from distributed_training_amd.resnet import micro_resnet
+
+    ddp = DistributedDataParallel(micro_resnet().to(cuda_device))
+    cal = xgmi_bucket_caps(ddp._calib_allreduce, 8)
+    assert [p["bytes"] for p in cal["points"]] == [m * 2**20 for m in (1, 4, 16, 64)]
+    assert all(p["ms"] > 0 for p in cal["points"])
+    assert 4 * 2**20 <= cal["bucket_cap_bytes"] <= 256 * 2**20
+    assert 256 * 1024 <= cal["last_bucket_cap_bytes"] <= cal["bucket_cap_bytes"]
