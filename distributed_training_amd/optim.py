@@ -67,11 +67,19 @@ class _PlanCache:
         return list(self._plans.values())
 
 
-def _check_dense(p: torch.Tensor, g: torch.Tensor, what: str):
+def _check_dense(p: torch.Tensor, g: torch.Tensor, what: str, seen: dict | None = None):
+    """p dense and g in p's layout.  ``seen`` (id(p) -> strides found dense)
+    skips the walk over the dims for a parameter already checked — a grad with
+    the same strides (and shape) is then dense too."""
+    ps = p.stride()
+    if g.stride() != ps:
+        raise RuntimeError(f"{what}: grad layout must match its parameter's (param {ps}, grad {g.stride()})")
+    if seen is not None and seen.get(id(p)) == ps:
+        return
     if not is_dense(p):
-        raise RuntimeError(f"{what}: parameters must be dense (got strides {p.stride()})")
-    if g.stride() != p.stride() or not is_dense(g):
-        raise RuntimeError(f"{what}: grad layout must match its parameter's (param {p.stride()}, grad {g.stride()})")
+        raise RuntimeError(f"{what}: parameters must be dense (got strides {ps})")
+    if seen is not None:
+        seen[id(p)] = ps
 
 
 class _FusedBase(torch.optim.Optimizer):
@@ -82,6 +90,7 @@ class _FusedBase(torch.optim.Optimizer):
         self.found_inf: torch.Tensor | None = None
         self._clip_buf: dict = {}
         self._dev_hyper: dict = {}  # param-group index -> device hyper-parameter buffers
+        self._dense_seen: dict = {}  # id(param) -> strides already checked dense
 
     @property
     def capturable(self) -> bool:
@@ -190,7 +199,7 @@ class FusedSGD(_FusedBase):
                 continue
             if p.grad.is_sparse:
                 raise RuntimeError("FusedSGD does not support sparse gradients")
-            _check_dense(p, p.grad, "FusedSGD")
+            _check_dense(p, p.grad, "FusedSGD", self._dense_seen)
             if p.dtype != torch.float32:
                 raise RuntimeError("FusedSGD expects fp32 parameters (keep a fp32 master copy)")
             st = self.state[p]
@@ -296,7 +305,7 @@ class FusedAdam(_FusedBase):
                     continue
                 if p.grad.is_sparse:
                     raise RuntimeError("FusedAdam does not support sparse gradients")
-                _check_dense(p, p.grad, "FusedAdam")
+                _check_dense(p, p.grad, "FusedAdam", self._dense_seen)
                 if p.dtype != torch.float32:
                     raise RuntimeError("FusedAdam expects fp32 parameters (keep a fp32 master copy)")
                 st = self.state[p]
