@@ -786,6 +786,9 @@ class DistributedDataParallel(nn.Module):
             raise RuntimeError(f"{optim} does not support overlapped DDP (SGD, Adam, AdamW)")
         if kwargs.get("max_grad_norm"):
             raise RuntimeError("overlapped optimizer: a global-norm clip needs every bucket before any update")
+        if self._found_inf_target is not None:
+            raise RuntimeError("overlapped optimizer: AMP loss scaling needs the overflow check of every bucket "
+                               "before any update (torch's overlapped optimizer has no GradScaler path either)")
         params = list(optim_params) if optim_params is not None else list(self._params)
         opt = cls(params, *args, **kwargs)
         self._overlap = {"cls": cls, "args": args, "kwargs": kwargs, "opt": opt, "ids": {id(p) for p in params},
@@ -810,6 +813,8 @@ class DistributedDataParallel(nn.Module):
         backward filled it)."""
         if t is not None and (t.numel() != 1 or t.dtype != torch.float32 or t.device != self.device):
             raise ValueError("found_inf target must be a 1-element float32 tensor on the DDP device")
+        if t is not None and self._overlap is not None:
+            raise RuntimeError("AMP loss scaling and the overlapped optimizer do not compose")
         self._found_inf_target = t
         self._found_inf_valid = False
         L.check(L.lib().gs_bucketer_set_found_inf(self._bucketer.handle, None if t is None else t.data_ptr()),
