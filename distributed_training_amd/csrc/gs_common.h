@@ -121,9 +121,10 @@ struct PlanArgs {
   const uint32_t* align;      // [n] bit s = slot s pointer is 16-B aligned
   const ChunkDesc* chunks;    // [n_chunks]
   const int64_t* voff;        // [n] virtual offsets (chunk-map engine)
-  uint32_t* ticket;           // arrival counter of the fused reduction (0 between launches)
+  uint32_t* ticket;           // arrival counters of the fused reduction (0 between launches)
   float* red_out;             // fused reduction target (chunk engine), NULL = none
   int32_t red_acc;            // accumulate into red_out
+  int32_t red_fuse;           // R > 0: combine in-kernel (two-level ticket, R groups), no combine launch
   int32_t per_wg;             // chunk engine: groups per workgroup (0 = grid-stride)
   int32_t n;
   int32_t n_tasks;
@@ -174,9 +175,9 @@ struct gs_plan {
   std::vector<uint32_t> h_align;   // [n]
   bool dirty = true;
   // device side (HIP plans only)
-  void* d_static = nullptr;  // segs | task_begin | numel | off | chunks | voff | ticket
+  void* d_static = nullptr;  // segs | task_begin | numel | off | chunks | voff
   void* d_table = nullptr;   // ptrs | align
-  float* d_partials = nullptr;  // [kGridLimit]
+  float* d_partials = nullptr;  // [kGridLimit] partials + the fused reduction's sync words
   void* pinned = nullptr;       // staging ring for table uploads
   int ring = 0;
   void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};

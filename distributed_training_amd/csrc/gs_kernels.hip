@@ -119,9 +119,20 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #endif
 // chunks per workgroup iteration (chunk-map engine), per op; measured in
 // profiles/r2*_kernels_*.jsonl (scripts/r2_engine_ab.sh)
-#ifndef GS_FUSED_RED
-#define GS_FUSED_RED 0  // 1: chunk-engine reductions combine in-kernel (ticket) — measured slower (r2c)
+// in-kernel combine of capped chunk-engine reductions (two-level ticket over
+// GS_RED_FUSE groups) instead of the combine_partials launch (0); the
+// environment variable of the same name overrides.
+// A single-counter ticket measured slower than the launch (r2c).
+#ifndef GS_RED_FUSE
+#define GS_RED_FUSE 64
 #endif
+#ifndef GS_RED_FUSE_GRID
+#define GS_RED_FUSE_GRID 2048  // workgroups of a fused reduction (r2z2 sweep: 2048 < 4096 < 8192)
+#endif
+constexpr int kRedMaxGroups = 64;
+constexpr int kRedSyncStride = 32;  // words: every counter / group sum on its own 128-B line
+constexpr int kRedSyncWords = (2 * kRedMaxGroups + 1) * kRedSyncStride;
+constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too many arrivals
 #ifndef GS_G_PACK
 #define GS_G_PACK 1     // fp32 bucket
 #endif
@@ -635,39 +646,72 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   if constexpr (Op::kRed != 0) {
     constexpr bool MAX = Op::kRed == 2;
     const float r = block_reduce<MAX>(acc);
-#if GS_FUSED_RED
-    // fused combine: the partial goes out write-through (agent-scope store),
-    // then the workgroup arrives on a device-scope ticket; the last to arrive
-    // reads every partial with agent-scope loads (L2-served, never a stale
-    // L1 line), combines them in combine_partials' fixed order and re-arms
-    // the ticket.  No release/acquire fences: MI355X_MICROARCH.md hand-off
-    // table, row 1 (sc1 stores, s_waitcnt vmcnt(0), atomic add, sc1 loads).
-    if (P.red_out == nullptr) return;  // uniform
-    __shared__ int s_last;
+    if (!P.red_fuse) {
+      if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+      return;
+    }
+    // In-kernel combine, two-level ticket.  Workgroup b belongs to group
+    // b mod R (R = P.red_fuse, a power of two <= kRedMaxGroups; with R a
+    // multiple of 8 a group's workgroups share the round-robin XCD of their
+    // dispatch: speed only, nothing assumes it).  Each group has its own
+    // arrival counter on its own 128-B line, so no device-scope word sees
+    // more than grid/R arrivals (one word serialises them at ~12 ns each —
+    // MI355X_MICROARCH.md "fanin"; the single-counter form measured 2.4 TB/s,
+    // r2c).  The partial goes out write-through (agent-scope store), the
+    // storing wave drains it (vmcnt(0)), then arrives; the group's last
+    // arriver folds the group's partials (agent-scope loads) in block order,
+    // publishes the group sum the same way and arrives on the top counter;
+    // the last group folds the R group sums in group order.  Every counter is
+    // re-armed by its last arriver.  The result depends only on the grid and
+    // R, not on arrival order: deterministic, so ranks reducing identical
+    // grads agree bit for bit.  Hand-off form: MI355X_MICROARCH.md's table,
+    // row 1 (sc1 stores, vmcnt(0), atomic add, sc1 loads), no fences.
+    constexpr int kStride = kRedSyncStride;
+    __shared__ int s_role;  // 0: done, 1: group leader, 2: also the last group
+    const int R = P.red_fuse;
+    const int k = static_cast<int>(blockIdx.x) & (R - 1);
+    const int grid = static_cast<int>(gridDim.x);
+    const int n_groups = grid < R ? grid : R;
+    uint32_t* top = &P.ticket[kRedMaxGroups * kStride];
+    float* gsums = reinterpret_cast<float*>(P.ticket + (kRedMaxGroups + 1) * kStride);
     if (threadIdx.x == 0) {
+      const uint32_t ng = static_cast<uint32_t>((grid - 1 - k) / R + 1);
       __hip_atomic_store(&op.partials[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t tk = __hip_atomic_fetch_add(P.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = tk == gridDim.x - 1;
+      const uint32_t tk = __hip_atomic_fetch_add(&P.ticket[k * kStride], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      s_role = tk == ng - 1;
     }
     __syncthreads();
-    if (s_last) {
-      float v = 0.f;
-      for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += kBlock) {
-        const float x = __hip_atomic_load(&op.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v = MAX ? fmaxf(v, x) : v + x;
-      }
-      const float tot = block_reduce<MAX>(v);
-      if (threadIdx.x == 0) {
-        float* out = P.red_out;
-        if (MAX) out[0] = P.red_acc ? fmaxf(out[0], tot) : tot;
-        else out[0] = P.red_acc ? out[0] + tot : tot;
-        __hip_atomic_store(P.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    if (!s_role) return;  // uniform within the workgroup
+    float v = 0.f;
+    for (int i = k + R * static_cast<int>(threadIdx.x); i < grid; i += R * kBlock) {
+      const float x = __hip_atomic_load(&op.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = MAX ? fmaxf(v, x) : v + x;
     }
-#else
-    if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
-#endif
+    const float gsum = block_reduce<MAX>(v);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&P.ticket[k * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gsums[k * kStride], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_role = tk == static_cast<uint32_t>(n_groups) - 1 ? 2 : 0;
+    }
+    __syncthreads();
+    if (s_role != 2 || threadIdx.x >= 64) return;
+    // the last group: wave 0 folds the group sums (lane j: group j, j + 64, ...)
+    float t = 0.f;
+    for (int j = static_cast<int>(threadIdx.x); j < n_groups; j += 64) {
+      const float x = __hip_atomic_load(&gsums[j * kStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = MAX ? fmaxf(t, x) : t + x;
+    }
+    const float tot = MAX ? wave_max(t) : wave_sum(t);
+    if (threadIdx.x == 0) {
+      float* out = P.red_out;
+      if (MAX) out[0] = P.red_acc ? fmaxf(out[0], tot) : tot;
+      else out[0] = P.red_acc ? out[0] + tot : tot;
+      __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -697,6 +741,18 @@ int red_grid_cap(int op_default) {
     return e ? std::max(1, std::min(std::atoi(e), kGridLimit)) : 0;
   }();
   return v > 0 ? v : op_default;
+}
+// in-kernel combine groups (0 = the combine_partials launch); GS_RED_FUSE=<R>
+int red_fuse_groups() {
+  static const int v = [] {
+    const char* e = std::getenv("GS_RED_FUSE");
+    int r = e ? std::atoi(e) : GS_RED_FUSE;
+    if (r <= 0) return 0;
+    int p2 = 1;
+    while (p2 < r && p2 < kRedMaxGroups) p2 <<= 1;
+    return p2;
+  }();
+  return v;
 }
 bool red_contiguous() {
   static const bool v = [] {
@@ -1081,22 +1137,27 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
   const bool chunk = use_chunk_engine(Op::kKind) && !p->chunks.empty();
   int grid = p->grid;
+  bool fused = false;
   if (chunk) {
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
     const bool red = Op::kRed != 0 && red_out;
-    const int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
+    int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
+    fused = red && cap <= kRedFuseMaxGrid && red_fuse_groups() > 0;
+    if (fused) cap = std::min(cap, red_grid_cap(GS_RED_FUSE_GRID));
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     PlanArgs a = p->args();
     a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
     a.red_out = Op::kRed != 0 ? red_out : nullptr;
     a.red_acc = accumulate;
+    a.red_fuse = fused ? red_fuse_groups() : 0;
+    a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
     hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
   } else {
     hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
   }
   HIP_RET(hipGetLastError());
   if constexpr (Op::kRed != 0) {
-    if (red_out && !(chunk && GS_FUSED_RED)) {
+    if (red_out && !fused) {
       hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s,
                          (const float*)p->d_partials, grid, red_out, accumulate);
       HIP_RET(hipGetLastError());
@@ -1153,11 +1214,11 @@ int hip_plan_upload_static(gs_plan* p) {
   const size_t sz_n = sizeof(int64_t) * p->n;
   const size_t sz_ch = sizeof(ChunkDesc) * p->chunks.size();
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  // segs | task_begin | numel | off | chunks | voff | ticket (layout of gs_plan::args)
-  const size_t total = al(sz_segs) + al(sz_tb) + al(sz_n) * 3 + al(sz_ch) + 256;
+  // segs | task_begin | numel | off | chunks | voff (layout of gs_plan::args)
+  const size_t total = al(sz_segs) + al(sz_tb) + al(sz_n) * 3 + al(sz_ch);
   HIP_RET(hipMalloc(&p->d_static, total));
   char* base = static_cast<char*>(p->d_static);
-  std::vector<char> h(total, 0);  // the ticket starts at 0; every fused reduction re-arms it
+  std::vector<char> h(total, 0);
   size_t o = 0;
   if (sz_segs) std::memcpy(h.data() + o, p->segs.data(), sz_segs);
   o += al(sz_segs);
@@ -1174,7 +1235,10 @@ int hip_plan_upload_static(gs_plan* p) {
   const size_t tb = table_bytes(p) + 16;
   HIP_RET(hipMalloc(&p->d_table, tb));
   HIP_RET(hipMemset(p->d_table, 0, tb));
-  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * kGridLimit));
+  // per-workgroup partials + the fused reduction's counters / group sums (zeroed once;
+  // every fused launch leaves them at zero)
+  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * (kGridLimit + kRedSyncWords)));
+  HIP_RET(hipMemset(p->d_partials + kGridLimit, 0, sizeof(float) * kRedSyncWords));
   HIP_RET(hipHostMalloc(&p->pinned, tb * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) {
     hipEvent_t ev;

@@ -50,9 +50,10 @@ gs::PlanArgs gs_plan::args() const {
   o += al(sizeof(ChunkDesc) * chunks.size());
   a.voff = reinterpret_cast<const int64_t*>(base + o);
   o += al(sizeof(int64_t) * n);
-  a.ticket = reinterpret_cast<uint32_t*>(base + o);
+  a.ticket = nullptr;  // the launch points it at the sync words after d_partials
   a.red_out = nullptr;
   a.red_acc = 0;
+  a.red_fuse = 0;
   a.per_wg = 0;
   a.ptrs = static_cast<void* const*>(d_table);
   a.align = reinterpret_cast<const uint32_t*>(static_cast<char*>(d_table) +
