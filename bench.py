@@ -71,8 +71,8 @@ def parse():
     ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: N>1 control-flow rehearsal with ranks sharing GPUs (not a measurement)")
     ap.add_argument("--impl", default="libgsync", choices=["libgsync", "torch"],
-                    help="torch = the reference path on the same GPU (torch DDP + torch.optim SGD/Adam foreach), "
-                         "for comparison; DDP engine only")
+                    help="torch = the reference path on the same GPU (torch DDP + torch.optim SGD/Adam foreach; "
+                         "with --engine colossal: + fp16 autocast, torch.amp.GradScaler, fused AdamW), for comparison")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: record the whole step (forward, backward + bucket sync, update) into one hipGraph "
                          "(CapturedStep, capturable optimizer) and replay it")
@@ -276,12 +276,19 @@ def main():
     n_params = sum(p.numel() for p in model.parameters())
     zero = None
     if args.impl == "torch":
-        if args.engine != "ddp" or args.graph:
-            raise SystemExit("--impl torch: DDP engine, eager only")
+        if args.engine not in ("ddp", "colossal") or args.graph:
+            raise SystemExit("--impl torch: DDP or colossal engine, eager only")
         ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[dev.index] if args.pg_backend == "nccl" else None,
             bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=args.grad_as_bucket_view)
-        if args.optimizer == "sgd":
+        if args.engine == "colossal":
+            # what Colossal's TorchDDPPlugin + mixed_precision='fp16' + HybridAdam run on torch alone:
+            # torch DDP, fp16 autocast (criterion inside), torch.amp.GradScaler, fused AdamW
+            # (HybridAdam(adamw_mode=True), weight_decay 0: R:resnet/colossal/colossal_train.py:118-161)
+            opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3 * world, weight_decay=0.0, fused=True)
+            torch_scaler = torch.amp.GradScaler("cuda")
+            bytes_per_param = 28
+        elif args.optimizer == "sgd":
             opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=True)
             bytes_per_param = 20
         else:
@@ -378,7 +385,16 @@ def main():
         opt_w.zero_grad()
         return loss
 
-    run = colossal_step if args.engine == "colossal" else train_step
+    def torch_colossal_step(xb, yb):  # the same step on torch's own DDP / GradScaler / fused AdamW
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = crit(ddp(xb), yb)
+        torch_scaler.scale(loss).backward()
+        torch_scaler.step(opt)
+        torch_scaler.update()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    run = (torch_colossal_step if args.impl == "torch" else colossal_step) if args.engine == "colossal" else train_step
     if args.graph:
         if zero is not None:
             raise SystemExit("--graph: DDP engine only")
@@ -572,7 +588,11 @@ def main():
         "dtype": "fp16" if args.engine == "colossal" else "bf16",
         "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
         "config": {
-            "workload": (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+            "workload": (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, "
+                         f"REFERENCE PATH for the Colossal config: torch DDP + torch.amp.GradScaler + "
+                         f"torch.optim.AdamW(fused=True) for comparison") if args.impl == "torch" and
+                        args.engine == "colossal" else
+                        (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
                          f"REFERENCE PATH torch DDP + torch.optim.{'SGD' if args.optimizer == 'sgd' else 'Adam'}"
                          f"(foreach) for comparison") if args.impl == "torch" else
                         (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, Colossal "
