@@ -275,9 +275,24 @@ def main():
     bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
     n_params = sum(p.numel() for p in model.parameters())
     zero = None
-    if args.impl == "torch":
+    torch_zero = args.impl == "torch" and args.engine == "zero2"
+    if torch_zero:
+        # configs[3] on torch alone: FSDP SHARD_GRAD_OP is ZeRO-2 (grads reduce-scattered, params
+        # replicated); bf16 compute / reduce-scatter over fp32 master shards as DeepSpeed's bf16
+        # mode; fused AdamW, clip 1.0 (R:resnet/deepspeed/deepspeed_train.py:170-219)
+        if args.graph:
+            raise SystemExit("--impl torch: eager only")
+        from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
+
+        bf = torch.bfloat16
+        ddp = FSDP(model, sharding_strategy=ShardingStrategy.SHARD_GRAD_OP, device_id=dev,
+                   mixed_precision=MixedPrecision(param_dtype=bf, reduce_dtype=bf, buffer_dtype=bf))
+        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3, weight_decay=3e-7, fused=True)
+        bytes_per_param = 28
+        grad_bytes = n_params * 2
+    elif args.impl == "torch":
         if args.engine not in ("ddp", "colossal") or args.graph:
-            raise SystemExit("--impl torch: DDP or colossal engine, eager only")
+            raise SystemExit("--impl torch: DDP, colossal or zero2 engine, eager only")
         ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[dev.index] if args.pg_backend == "nccl" else None,
             bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=args.grad_as_bucket_view)
@@ -350,7 +365,7 @@ def main():
 
     ev_opt = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
-    if zero is not None:
+    if zero is not None or torch_zero:
         x = x.to(torch.bfloat16)
 
     def step(i=None):
@@ -394,7 +409,16 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
-    run = (torch_colossal_step if args.impl == "torch" else colossal_step) if args.engine == "colossal" else train_step
+    def torch_zero_step(xb, yb):  # FSDP(SHARD_GRAD_OP) step: bf16 forward/backward, clip, fused AdamW
+        loss = crit(ddp(xb).float(), yb)
+        loss.backward()
+        ddp.clip_grad_norm_(1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    run = (torch_colossal_step if args.impl == "torch" else colossal_step) if args.engine == "colossal" else \
+        torch_zero_step if torch_zero else train_step
     if args.graph:
         if zero is not None:
             raise SystemExit("--graph: DDP engine only")
@@ -540,7 +564,10 @@ def main():
                                          "launches of this command (the event pair adds the kernel's dispatch)"}
         except Exception:
             trace_check = None
-    if args.impl == "torch":
+    if torch_zero:
+        log = {"has_rebuilt_buckets": 0}
+        bucket_bytes = []
+    elif args.impl == "torch":
         log = ddp._get_ddp_logging_data()
         bucket_bytes = [int(b) for b in str(log.get("rebuilt_bucket_sizes", "")).split(",") if b.strip()]
     elif zero is None:
@@ -588,7 +615,10 @@ def main():
         "dtype": "fp16" if args.engine == "colossal" else "bf16",
         "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
         "config": {
-            "workload": (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, "
+            "workload": (f"{args.model} synthetic 224x224 bf16 training, {args.batch} img/GPU, REFERENCE PATH for "
+                         f"the ZeRO-2 config: torch FSDP(SHARD_GRAD_OP, bf16 MixedPrecision) + clip 1.0 + "
+                         f"torch.optim.AdamW(fused=True) for comparison") if torch_zero else
+                        (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, "
                          f"REFERENCE PATH for the Colossal config: torch DDP + torch.amp.GradScaler + "
                          f"torch.optim.AdamW(fused=True) for comparison") if args.impl == "torch" and
                         args.engine == "colossal" else
