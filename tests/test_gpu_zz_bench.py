@@ -72,7 +72,9 @@ def _check_line(d, n):
     # the self-check step after the timed region (distributed_training_amd/parity.py)
     p = d["parity"]
     assert p is not None and p["ok"] is True and p["world"] == n, p
-    assert p["averaged_grads"]["bitwise_equal"] is True and p["weights_identical"] is True
+    assert p["averaged_grads"]["ok"] is True and p["weights_identical"] is True
+    if n <= 2:  # bitwise at ws <= 2, the 4(n-1)*2^-24*sum|g|/n bound above
+        assert p["averaged_grads"]["bitwise_equal"] is True
     assert p["buffers_identical"] is True
 
 
@@ -142,3 +144,30 @@ def test_bench_collective_bench_leg(cuda_device, engine):
     assert all(r["median_ms"] > 0 for r in sb["per_op"])
     assert sb["xgmi_peak_GBps"] == 0 and sb["frac"] is None  # one rank: no link in use
     assert d["parity"]["ok"] is True and d["parity"]["collective"] == "rccl(libgsync)", d["parity"]
+
+
+@pytest.mark.parametrize("engine,n", [("ddp", 4), ("zero2", 3)])
+def test_bench_multirank_gloo_rehearsal(cuda_device, engine, n):
+    """More ranks than the N=2 rehearsal, as the driver's 4/8-GPU runs: DDP at 4
+    ranks (the parity step's ws > 2 tolerance path, rank order != the
+    collective's order) and ZeRO-2 at 3 ranks (shards of a flat buffer padded
+    to 3 x 64 elements; reduce-scatter / all-gather over the rehearsal group)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "bench.py", "--gpus", str(n), "--pg-backend", "gloo", "--kernel-rates", "0"] + SMALL
+    if engine == "zero2":
+        cmd += ["--engine", "zero2"]
+    p = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}" and d["config"]["global_batch"] == 16 * n
+    assert abs(d["value"] - n * 16 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    par = d["parity"]
+    assert par["ok"] is True and par["world"] == n and par["collective"] == "gloo", par
+    assert par["averaged_grads"]["ok"] is True and par["weights_identical"] is True
+    if engine == "zero2":
+        assert d["roofline"]["algorithmic_bytes_per_launch"] == 20 * (d["config"]["params"] // n)
+    else:
+        assert par["buffers_identical"] is True
