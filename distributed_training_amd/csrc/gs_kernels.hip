@@ -51,7 +51,14 @@ __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   __builtin_memcpy(&x, &h, 2);
   return static_cast<float>(x);
 }
+// fp32 -> fp16, round-to-nearest-even of the fp32 VALUE (torch: opmath in fp32,
+// then the cast).  The empty asm pins f as an fp32 register value: without it
+// LLVM folds the producing fma / mul into v_fma_mixlo_f16, which rounds the
+// exact result once, straight to fp16 — a different fp16 wherever the fp32
+// rounding lands on an fp16 tie (ZeRO fp16 params, fp16 buckets, fp16 unscale;
+// found as master.half() != the fp16 param in test_colossal_low_level_zero_fp16_gpu)
 __device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  __asm__("" : "+v"(f));
   _Float16 x = static_cast<_Float16>(f);
   uint16_t h;
   __builtin_memcpy(&h, &x, 2);

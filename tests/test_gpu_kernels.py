@@ -283,3 +283,56 @@ def test_plan_launch_timer(cuda_device):
     plan.timer_enable(0)
     plan.sgd(torch.float32, 1e-3, 0.9, 0.0, 0.0, False, False, False)
     assert plan.timer_read() == []
+
+
+def test_fp16_outputs_round_the_fp32_value(cuda_device):
+    """Every fp16 output is the round-to-nearest-even of the fp32 result, as
+    torch's opmath-then-cast: pack ×s into an fp16 bucket == (x * s).half(),
+    the in-place fp16 unscale == (g.float() * inv).half(), the fused update's
+    fp16 param copy == the fp32 master's .half().  (LLVM folded the producing
+    fma / mul into v_fma_mixlo_f16 — one rounding, straight to fp16 — which
+    differs wherever the fp32 value is an fp16 tie: ~1e-4 of random inputs.)"""
+    from distributed_training_amd.multi_tensor import TensorListPlan, update_task_units
+
+    dev = cuda_device
+    n = 1 << 20
+    g = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(n, device=dev, generator=g)
+    s = float(np.float32(1.0 / 3.0))
+    plan = TensorListPlan([n], dev, align=64)
+    plan.set_ptrs(1, [x])
+    flat = torch.zeros(plan.flat_numel, dtype=torch.float16, device=dev)
+    plan.pack(1, torch.float32, flat, s, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(flat[:n], (x * s).half())
+
+    g16 = (torch.randn(n, device=dev, generator=g) * 100).half()
+    inv = torch.tensor([s], device=dev)
+    want = (g16.float() * inv).half()
+    p2 = TensorListPlan([n], dev)
+    p2.set_ptrs(1, [g16])
+    found = torch.zeros(1, device=dev)
+    p2.unscale_check(1, torch.float16, inv, found)
+    torch.cuda.synchronize()
+    assert found.item() == 0.0 and torch.equal(g16, want)
+
+    for kind in ("adam", "sgd"):
+        up = TensorListPlan([n], dev, task_units=update_task_units(dev))
+        p = torch.randn(n, device=dev, generator=g)
+        gr = torch.randn(n, device=dev, generator=g) * 1e-2
+        m = torch.zeros(n, device=dev)
+        v = torch.zeros(n, device=dev)
+        p16 = torch.zeros(n, device=dev, dtype=torch.float16)
+        up.set_ptrs(0, [p])
+        up.set_ptrs(1, [gr])
+        up.set_ptrs(2, [m])
+        if kind == "adam":
+            up.set_ptrs(3, [v])
+            up.set_ptrs(4, [p16])
+            up.adam(torch.float32, 1e-3, 0.9, 0.999, 1e-8, 0.0, True, False, -1e-3 / 0.1, 0.001 ** 0.5,
+                    lowp_dtype=torch.float16)
+        else:
+            up.set_ptrs(3, [p16])
+            up.sgd(torch.float32, 0.1, 0.9, 0.0, 1e-4, False, False, True, lowp_dtype=torch.float16)
+        torch.cuda.synchronize()
+        assert torch.equal(p16, p.half()), f"{kind}: {(p16 != p.half()).sum().item()} of {n}"

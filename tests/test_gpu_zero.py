@@ -212,3 +212,65 @@ def test_deepspeed_checkpoint_resume_gpu(cuda_device, rccl_pg, tmp_path):
         assert torch.equal(a, b), n
     sd = e1.consolidated_fp32_state_dict()
     assert list(sd) == list(m1.state_dict())
+
+
+def test_colossal_low_level_zero_fp16_gpu(cuda_device, rccl_pg):
+    """The reference's `-p low_level_zero` plugin (R:resnet/colossal/colossal_train.py:135-136,
+    LowLevelZeroPlugin(initial_scale=2**5): ZeRO-1, fp16 model, fp32 master, dynamic loss
+    scale 32) through the Colossal shim on the GPU (RCCL ws=1), two steps, against a torch
+    restatement of the same arithmetic: (loss·32).backward() on the fp16 model, grads ×1/32
+    into fp32, torch AdamW (HybridAdam's adamw_mode, wd 0) on an fp32 master, fp16 copy back.
+    fp32 masters within SURVEY §8c's Adam bound lr·1e-3 (observed 3e-8); our fp16 params ==
+    master.half().  Two steps, not more: a master difference of a few ulp flips the fp16
+    rounding of ~1e-3 of the elements, after which fp16 training diverges chaotically on
+    both sides (scripts/llz_diag.py: 3e-8 after step 2, 1.3e-3 after step 3).  MIOpen in
+    deterministic mode so both sides see the same conv results."""
+    sys.path.insert(0, SHIMS)
+    import colossalai  # noqa: F401
+    from colossalai.booster import Booster
+    from colossalai.booster.plugin import LowLevelZeroPlugin
+    from colossalai.nn.optimizer import HybridAdam
+
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        lr = 1e-3
+        torch.manual_seed(0)
+        model = _micro().to(cuda_device)
+        ref16 = _micro().to(cuda_device)
+        ref16.load_state_dict(model.state_dict())
+        ref16 = ref16.half()
+        master = [p.detach().float().clone().requires_grad_() for p in ref16.parameters()]
+        ropt = torch.optim.AdamW(master, lr=lr, weight_decay=0.0, foreach=False)
+        booster = Booster(plugin=LowLevelZeroPlugin(initial_scale=2 ** 5))
+        crit = nn.CrossEntropyLoss()
+        bmodel, bopt, bcrit, _, _ = booster.boost(model, HybridAdam(model.parameters(), lr=lr), criterion=crit)
+        assert bopt.zero.scaler.scale == 32.0 and bopt.zero.stage == 1
+        for it in range(2):
+            g = torch.Generator(device=cuda_device).manual_seed(100 + it)
+            x = torch.rand(8, 3, 32, 32, device=cuda_device, generator=g)
+            y = torch.randint(0, 10, (8,), device=cuda_device, generator=g)
+            loss = bcrit(bmodel(x), y)
+            booster.backward(loss, bopt)
+            bopt.step()
+            bopt.zero_grad()
+            # the restatement
+            (crit(ref16(x.half()).float(), y).float() * 32.0).backward()
+            with torch.no_grad():
+                for m, p in zip(master, ref16.parameters()):
+                    m.grad = p.grad.float() * (1.0 / 32.0)
+                    p.grad = None
+            ropt.step()
+            with torch.no_grad():
+                for m, p in zip(master, ref16.parameters()):
+                    p.copy_(m.half())
+            torch.cuda.synchronize()
+            mine = bopt.zero.consolidated_state_dict()
+            for (n, p16), m in zip(model.named_parameters(), master):
+                got = mine[n].to(cuda_device).float()
+                err = (got - m.detach()).abs().max().item()
+                assert err <= lr * 1e-3, f"step {it + 1} {n}: max|Δ| {err}"
+                assert p16.dtype == torch.float16 and torch.equal(p16.detach(), got.half()), n
+        assert bopt.zero.scaler.scale == 32.0  # no overflow, no growth within 1000 steps
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
