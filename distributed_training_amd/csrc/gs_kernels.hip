@@ -336,16 +336,30 @@ __device__ __forceinline__ bool slot_vec(const PlanArgs& P, int slot, int t) {
 }
 
 // ------------------------------------------------------- wave/block reduce
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// DPP wave reduction (GFX9 DPP, all in VALU — no LDS crossbar): quad swaps,
+// half-row and row mirrors give every lane its row-of-16 total, row_bcast:15
+// folds rows 0->1 and 2->3, row_bcast:31 folds row 1 into rows 2-3, so lane
+// 63 holds the wave total; v_readlane broadcasts it.  A fixed tree:
+// deterministic.  Lanes of rows a DPP op does not write keep `id`.
+template <int Ctrl, int RowMask, bool MAX>
+__device__ __forceinline__ float dpp_op(float v, float id) {
+  const int s = __builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), Ctrl, RowMask, 0xF, false);
+  const float t = __int_as_float(s);
+  return MAX ? fmaxf(v, t) : v + t;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce(float v) {
+  const float id = MAX ? -INFINITY : 0.f;
+  v = dpp_op<0xB1, 0xF, MAX>(v, id);   // quad_perm [1,0,3,2]
+  v = dpp_op<0x4E, 0xF, MAX>(v, id);   // quad_perm [2,3,0,1]
+  v = dpp_op<0x141, 0xF, MAX>(v, id);  // row_half_mirror
+  v = dpp_op<0x140, 0xF, MAX>(v, id);  // row_mirror
+  v = dpp_op<0x142, 0xA, MAX>(v, id);  // row_bcast:15 into rows 1, 3
+  v = dpp_op<0x143, 0xC, MAX>(v, id);  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+__device__ __forceinline__ float wave_sum(float v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v); }
 // block of kBlock threads; result valid in thread 0
 template <bool MAX>
 __device__ __forceinline__ float block_reduce(float v) {
