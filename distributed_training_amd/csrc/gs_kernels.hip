@@ -608,6 +608,46 @@ __device__ __forceinline__ void chunk_mixed(const Op& op, const PlanArgs& P, int
   op.template apply<false>(v, local, 0u, f, acc);
 }
 
+// The same with the span's descriptors staged in LDS (the north star's "LDS
+// staging for small-tensor gather"): the first `span` lanes each load one
+// tensor's extent [voff, voff + numel) and its descriptor (stream pointers,
+// alignment bits) into LDS, then every lane binary-searches LDS instead of
+// chasing log2(span) dependent global loads and reads its tensor's descriptor
+// from LDS instead of gathering it.  Runs of small tensors (BN weights /
+// biases, tensor tails) are the chunks this serves; spans above kMixedStage
+// (runs of tiny or empty tensors) keep the global path.  The caller's branch
+// is uniform across the workgroup (the chunk's code), so the barriers are too.
+// Measured: profiles/r2mlds/ (tiny tensors pack -15 %, R50 neutral).
+#ifndef GS_MIXED_LDS
+#define GS_MIXED_LDS 1
+#endif
+constexpr int kMixedStage = 64;  // tensors per mixed chunk staged (5 KB of LDS)
+template <class Op>
+__device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
+                                                float& acc, int64_t* s_lo, int64_t* s_hi, TV* s_tv) {
+  __syncthreads();  // the previous mixed chunk's lanes are done with the stage
+  if (static_cast<int>(threadIdx.x) < span) {
+    const int t = t0 + static_cast<int>(threadIdx.x);
+    const TV d = load_tv<false>(op, P, t);
+    s_lo[threadIdx.x] = P.voff[t];
+    s_hi[threadIdx.x] = P.voff[t] + d.numel;
+    s_tv[threadIdx.x] = d;
+  }
+  __syncthreads();
+  const int64_t e = c * kChunkElems + static_cast<int>(threadIdx.x) * kUnit;
+  int lo = 0, hi = span - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_lo[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  const int64_t local = e - s_lo[lo];
+  if (local < 0 || e >= s_hi[lo]) return;  // alignment gap between tensors
+  const TV v = s_tv[lo];
+  typename Op::Frag f;
+  op.template load<false>(v, local, 0u, f);
+  op.template apply<false>(v, local, 0u, f, acc);
+}
+
 template <int G, class Op>
 __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int t, int64_t c0, float& acc) {
   // G chunks c0 .. c0+G-1, all inside tensor t
@@ -637,6 +677,8 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   float acc = 0.f;
   if (!op.active()) return;  // uniform across the grid
   load_hyper(op);            // uniform: graph-replayable lr / bias corrections
+  __shared__ int64_t s_lo[kMixedStage], s_hi[kMixedStage];  // mixed chunks: the span's extents
+  __shared__ TV s_tv[kMixedStage];                            // ... and descriptors
   const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
   const int* cw = &P.chunks[0].t0;  // [t0, code] pairs
   // groups per workgroup: grid-stride (per_wg == 0) or a contiguous range
@@ -661,6 +703,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
       const int tj = j == 0 ? t : cload(cw, 2 * c);
       const int cj = j == 0 ? code : cload(cw, 2 * c + 1);
       if (cj == 0) chunk_full<1>(op, P, tj, c, acc);
+      else if (GS_MIXED_LDS && cj > 0 && cj <= kMixedStage) chunk_mixed_lds(op, P, tj, cj, c, acc, s_lo, s_hi, s_tv);
       else if (cj > 0) chunk_mixed(op, P, tj, cj, c, acc);
     }
   }
