@@ -413,3 +413,45 @@ def test_overlapped_optimizer_ws1_rccl(cuda_device, rccl_pg, kind):
     assert all(s == comm.value for s in streams[:-1])  # updates under backward, on the comm stream
     # the tail runs on the producer stream (here the default stream, handle 0)
     assert (streams[-1] or 0) == (torch.cuda.current_stream(cuda_device).cuda_stream or 0)
+
+
+def test_mixed_dtype_buckets_ws1_rccl(cuda_device, rccl_pg):
+    """fp32 body + bf16 head + fp16 bias on the GPU (RCCL ws=1): the HIP path
+    of per-dtype buckets (pack / all-reduce / unpack per bucket dtype, rebuilt
+    in ready order) gives the same grads as torch's own DDP bit for bit, and
+    the same rebuilt bucket sizes (tests/test_ddp_mixed_dtype_cpu.py on CPU).
+    MIOpen in deterministic mode so both see identical local grads."""
+    from distributed_training_amd import DistributedDataParallel
+    from tests.test_ddp_mixed_dtype_cpu import Mixed
+
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        out = {}
+        for impl in ("torch", "libgsync"):
+            torch.manual_seed(0)
+            model = Mixed().to(cuda_device)
+            ddp = (torch.nn.parallel.DistributedDataParallel(model, device_ids=[cuda_device.index])
+                   if impl == "torch" else DistributedDataParallel(model))
+            g = torch.Generator(device=cuda_device).manual_seed(1234)
+            grads = []
+            for _ in range(3):  # iteration 0: one bucket per dtype; then rebuilt in ready order
+                x = torch.rand(4, 3, 32, 32, device=cuda_device, generator=g)
+                y = torch.randint(0, 7, (4,), device=cuda_device, generator=g)
+                for p in model.parameters():
+                    p.grad = None
+                torch.nn.functional.cross_entropy(ddp(x), y).backward()
+                torch.cuda.synchronize()
+                grads.append([p.grad.clone() for p in model.parameters()])
+            sizes = ddp._get_ddp_logging_data()["rebuilt_bucket_sizes"]
+            out[impl] = (grads, sizes, ddp)
+        (tg, ts, _), (mg, ms, mddp) = out["torch"], out["libgsync"]
+        for it, (a, b) in enumerate(zip(tg, mg)):
+            for i, (u, v) in enumerate(zip(a, b)):
+                assert u.dtype == v.dtype and torch.equal(u, v), f"iter {it} param {i} ({u.dtype})"
+        ts = [int(v) for v in str(ts).split(",")] if isinstance(ts, str) else list(ts)
+        assert sorted(ts) == sorted(ms), (ts, ms)
+        assert set(mddp._bucketer.bucket_dtypes) == {torch.float32, torch.bfloat16, torch.float16}
+        assert all(b.is_cuda for b in mddp._bucketer.buffers)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
