@@ -682,6 +682,9 @@ def main():
         "parity": parity,
         **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
         "warmup_s": warm_s,
+        "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,
+                   "reserved_GB": torch.cuda.memory_reserved(dev) / 2**30,
+                   "device_total_GB": torch.cuda.get_device_properties(dev).total_memory / 2**30},
         "has_rebuilt_buckets": log.get("has_rebuilt_buckets", 0),
     }
     if args.cpu_baseline and world == 1:
