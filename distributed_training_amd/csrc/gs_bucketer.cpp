@@ -294,6 +294,10 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
   // div_factor is the world size (DDP / ZeRO divide by it); without a
   // communicator (host / external collectives) it is the only source of it
   const int world = comm ? gs_comm_world(comm) : std::max(1, static_cast<int>(div_factor + 0.5f));
+  static const int bucket_grid = [] {
+    const char* e = std::getenv("GSYNC_BUCKET_GRID");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
   for (int bi = 0; bi < n_buckets; ++bi) {
     Bucket& bk = b->buckets[bi];
     std::vector<int64_t> nm;
@@ -316,6 +320,12 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     }
     rc = gs_plan_create(device_kind, device, 1, &bk.numel, 0, &bk.flat);
     if (rc != GS_OK) return bail(rc);
+    if (bucket_grid > 0) {  // GSYNC_BUCKET_GRID: workgroups of the in-step bucket kernels (A/B runs)
+      for (gs_plan* q : {bk.plan, bk.flat}) {
+        q->grid_cap = std::min(q->grid_cap, bucket_grid);
+        q->grid = std::min(q->grid, bucket_grid);
+      }
+    }
     bk.pending = static_cast<int>(bk.params.size());
     bk.gdt = grad_dtype;
     bk.bdt = bucket_dtype;
