@@ -552,21 +552,36 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
 }
 
 // deterministic combine of the per-workgroup partials (fixed order): 1024
-// threads, thread t folds partials t, t+1024, ... in that order with 16 loads
-// issued before the first add, then a fixed-tree block reduction
+// threads, thread t folds the float4s t, t+1024, ... (8 16-B loads issued
+// before the first add: up to 32 Ki partials — the uncapped unpack + Σg² grid
+// of a ResNet-50 — in one round trip), the < 4 trailing partials go to threads
+// 0-2, then a fixed-tree block reduction
 constexpr int kCombineBlock = 1024;
 template <bool MAX>
 __global__ void __launch_bounds__(kCombineBlock) combine_partials(const float* partials, int n,
                                                                   float* out, int accumulate) {
   __shared__ float s_red[kCombineBlock / 64];
   float v = 0.f;
-  for (int i = threadIdx.x; i < n; i += 16 * kCombineBlock) {
-    float x[16];
+  const int n4 = n >> 2;
+  const float4* p4 = reinterpret_cast<const float4*>(partials);  // hipMalloc'd: 16-B aligned
+  for (int i = threadIdx.x; i < n4; i += 8 * kCombineBlock) {
+    float4 x[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = (i + u * kCombineBlock < n) ? partials[i + u * kCombineBlock] : 0.f;
+    for (int u = 0; u < 8; ++u)
+      x[u] = (i + u * kCombineBlock < n4) ? p4[i + u * kCombineBlock] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (i + u * kCombineBlock < n) v = MAX ? fmaxf(v, x[u]) : v + x[u];
+    for (int u = 0; u < 8; ++u) {
+      if (i + u * kCombineBlock < n4) {
+        v = MAX ? fmaxf(v, x[u].x) : v + x[u].x;
+        v = MAX ? fmaxf(v, x[u].y) : v + x[u].y;
+        v = MAX ? fmaxf(v, x[u].z) : v + x[u].z;
+        v = MAX ? fmaxf(v, x[u].w) : v + x[u].w;
+      }
+    }
+  }
+  if (static_cast<int>(threadIdx.x) < (n & 3)) {
+    const float x = partials[4 * n4 + threadIdx.x];
+    v = MAX ? fmaxf(v, x) : v + x;
   }
   v = MAX ? wave_max(v) : wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
