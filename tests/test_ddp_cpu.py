@@ -53,6 +53,20 @@ def _wrap(fn, rank, ws, port, errq, *args):
 
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+    _exit_ok()
+
+
+def _exit_ok():
+    """End a worker that finished cleanly without interpreter finalisation:
+    torch's gloo teardown at exit occasionally aborts ("terminate called
+    without an active exception", exit -6, about 1 run in 40 under load) after
+    every check has passed; the result is already reported, so skip it."""
+    import os
+    import sys
+
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 def _golden_run(rank, ws, name, use_torch_opt, hook):
