@@ -383,7 +383,11 @@ def main():
 
     def train_step(xb, yb):
         if args.graph:
-            opt.zero_grad(set_to_none=False)  # recorded grads are reused across replays
+            # released before every eager warm-up step and before the recording: the
+            # recorded backward then writes fresh grads in the graph's pool, reused by
+            # every replay (set_to_none=False would record a zero fill + an accumulate
+            # per parameter: ~1 ms a step at ResNet-50, profiles/r2graph/)
+            opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = ddp(xb)
             loss = crit(out, yb)

@@ -32,7 +32,10 @@ What stays correct across replays:
 Requirements are torch.cuda.graph's: static shapes (the same batch size on
 every call — a ragged last batch runs eagerly), no host synchronisation inside
 the step (``loss.item()`` belongs outside), and a ``zero_grad`` inside the
-step (or grads overwritten by backward) so that recorded grads are reused.
+step so that recorded grads are reused: `zero_grad(set_to_none=True)` at the
+start of the step is the cheap form (the recorded backward then writes fresh
+grads in the graph pool; `set_to_none=False` records a fill + an accumulate
+per parameter).
 DDP with ``find_unused_parameters=True`` or a comm hook that waits on the host
 is not capturable.
 """

@@ -53,7 +53,7 @@ def main():
             opt = D.FusedAdam(ddp.parameters(), lr=1e-3, capturable=impl == "graph")
 
         def train(xb, yb):
-            opt.zero_grad(set_to_none=impl != "graph")
+            opt.zero_grad(set_to_none=True)
             loss = crit(ddp(xb), yb)
             loss.backward()
             opt.step()

@@ -102,8 +102,12 @@ def rccl_pg(cuda_device):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("set_to_none", [False, True])
 @pytest.mark.parametrize("opt_name", ["sgd", "adam"])
-def test_captured_ddp_step_tracks_eager(cuda_device, rccl_pg, opt_name):
+def test_captured_ddp_step_tracks_eager(cuda_device, rccl_pg, opt_name, set_to_none):
+    """set_to_none=True: the grads are released at the start of every eager
+    step and of the recording, so the recorded backward writes fresh grads in
+    the graph's pool (no zero fill + accumulate per parameter on replay)."""
     import torch.nn as nn
 
     import distributed_training_amd as D
@@ -123,7 +127,7 @@ def test_captured_ddp_step_tracks_eager(cuda_device, rccl_pg, opt_name):
         crit = nn.CrossEntropyLoss()
 
         def train_step(x, y):
-            opt.zero_grad(set_to_none=False)
+            opt.zero_grad(set_to_none=set_to_none)
             loss = crit(ddp(x), y)
             loss.backward()
             opt.step()
