@@ -274,3 +274,13 @@ def test_colossal_low_level_zero_fp16_gpu(cuda_device, rccl_pg):
         assert bopt.zero.scaler.scale == 32.0  # no overflow, no growth within 1000 steps
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+
+
+def test_zero2_dynamic_loss_scaling_overflow_gpu_fp16(cuda_device, rccl_pg):
+    """The DeepSpeed fp16 path (R:resnet/deepspeed/deepspeed_train.py:200-208) on the
+    GPU: fp16 model, ZeRO-2 over RCCL, an overflowing step skipped without touching
+    params / masters / the step count, hysteresis then halving of the scale
+    (tests/test_zero_cpu.py::_zero_overflow, also run there at ws=2)."""
+    from tests.test_zero_cpu import _zero_overflow
+
+    _zero_overflow(0, 1, cuda_device, torch.float16)

@@ -69,3 +69,48 @@ def test_zero_with_clipping_ws3():
 
 def test_zero_bf16_model_replicas_agree():
     _run(_zero_vs_ddp, 2, 2, "adamw", 1.0, "bf16")
+
+
+def _zero_overflow(rank, ws, device="cpu", dtype=torch.float32):
+    """DeepSpeed-style dynamic loss scaling through ZeRO-2 (R:resnet/deepspeed/
+    deepspeed_train.py:200-208, loss_scale 0 = dynamic, hysteresis 2): an
+    overflow on ONE rank skips the step on every rank (the reduce-scattered
+    shards carry it; the found-inf flag is all-reduced), leaves params, fp32
+    masters and the step count untouched; the first overflow only spends the
+    hysteresis, the second in a row halves the scale; clean steps update."""
+    from distributed_training_amd.zero import DynamicLossScaler, ZeroDataParallel
+
+    torch.manual_seed(0)
+    m = _micro().to(device).to(dtype)
+    scaler = DynamicLossScaler(init_scale=2.0 ** 8, scale_window=1000, hysteresis=2)
+    z = ZeroDataParallel(m, stage=2, optimizer="adamw", lr=1e-3, loss_scaler=scaler)
+    g = torch.Generator(device=device).manual_seed(7 + rank)
+    want = [  # (poison on, step taken, scale after, step count after)
+        ("none", True, 256.0, 1), ("rank0", False, 256.0, 1), ("all", False, 128.0, 1), ("none", True, 128.0, 2)]
+    for it, (poison, taken, scale_after, steps_after) in enumerate(want):
+        x = torch.rand(4, 3, 32, 32, device=device, generator=g).to(dtype)
+        y = torch.randint(0, 10, (4,), device=device, generator=g)
+        before = [p.detach().clone() for p in m.parameters()]
+        master_before = torch.cat([t.detach().reshape(-1) for t in z.master]).clone()
+        z.prepare_backward()
+        loss = nn.functional.cross_entropy(m(x).float(), y)
+        if poison == "all" or (poison == "rank0" and rank == 0):
+            loss = loss * float("inf")
+        (loss * scaler.scale).backward()
+        ok = z.step()
+        z.zero_grad()
+        master_after = torch.cat([t.detach().reshape(-1) for t in z.master])
+        changed = any(not torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+        assert ok == taken and changed == taken, (it, ok, changed)
+        assert torch.equal(master_before, master_after) != taken, it
+        assert scaler.scale == scale_after and z.step_count == steps_after, (it, scaler.scale, z.step_count)
+    w = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()])
+    if ws > 1:
+        allw = [torch.zeros_like(w) for _ in range(ws)]
+        dist.all_gather(allw, w)
+        assert all(torch.equal(allw[0], o) for o in allw[1:])
+    z.close()
+
+
+def test_zero2_dynamic_loss_scaling_overflow_skip_ws2():
+    _run(_zero_overflow, 2)
