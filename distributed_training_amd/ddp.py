@@ -492,8 +492,15 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _sync_module_states(self):
-        """_sync_module_states: params + buffers from rank 0 (T:nn/parallel/distributed.py:860-870)."""
-        self._broadcast_tensors([p.detach() for p in self._params] + self._module_buffers())
+        """_sync_module_states: params + buffers from rank 0 (T:nn/parallel/distributed.py:860-870).
+        Every parameter, frozen ones included (torch's ``module_states`` walks
+        ``named_parameters()`` without a requires_grad filter)."""
+        seen, params = set(), []
+        for p in self.module.parameters():
+            if id(p) not in seen:
+                seen.add(id(p))
+                params.append(p.detach())
+        self._broadcast_tensors(params + self._module_buffers())
 
     @torch.no_grad()
     def _sync_buffers(self):

@@ -211,3 +211,38 @@ def _state_dict_keys(rank, ws):
 
 def test_state_dict_has_module_prefix():
     _run(_state_dict_keys, 1)
+
+
+def _frozen(rank, ws):
+    """A frozen layer (requires_grad=False): torch's DDP leaves it out of the
+    buckets but still broadcasts it from rank 0 at wrap time; grads of the
+    trainable ones equal torch DDP's bit for bit."""
+    import distributed_training_amd as D
+
+    out = {}
+    for impl in ("torch", "libgsync"):
+        torch.manual_seed(0)
+        model = _micro()
+        torch.manual_seed(100 + rank)  # ranks start with different frozen weights
+        with torch.no_grad():
+            model.conv1.weight.normal_()
+        model.conv1.weight.requires_grad_(False)
+        ddp = (torch.nn.parallel.DistributedDataParallel(model) if impl == "torch"
+               else D.DistributedDataParallel(model))
+        g = torch.Generator().manual_seed(1234 + rank)
+        x = torch.rand(4, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        torch.nn.functional.cross_entropy(ddp(x), y).backward()
+        out[impl] = (model.conv1.weight.detach().clone(),
+                     [p.grad.clone() if p.grad is not None else None for p in model.parameters()])
+    (tw, tg), (mw, mg) = out["torch"], out["libgsync"]
+    assert torch.equal(tw, mw)  # rank 0's frozen weights on every rank
+    w = [torch.zeros_like(mw) for _ in range(ws)]
+    dist.all_gather(w, mw)
+    assert all(torch.equal(w[0], o) for o in w[1:])
+    for a, b in zip(tg, mg):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
+
+
+def test_frozen_parameters_broadcast_and_grads_match_torch():
+    _run(_frozen, 2)
