@@ -248,20 +248,28 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    init_method = None  # env:// (torch.distributed.run's store) at N > 1
     if world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        # one rank: a file store — no TCP port to race for (a port picked free can be
+        # taken by another process's ephemeral socket before the store listens on it)
+        import tempfile
+
+        store_path = os.path.join(tempfile.gettempdir(), f"gsync_bench_{os.getpid()}_{time.time_ns()}")
+        init_method = "file://" + store_path
+        import atexit
+
+        atexit.register(lambda: os.path.exists(store_path) and os.remove(store_path))
     if args.pg_backend == "gloo":
         # rehearsal of the N > 1 control flow on a box with fewer GPUs than ranks:
         # ranks share the devices round-robin and the bucket collectives go through
         # gloo (RCCL refuses two ranks on one GPU); never the measured configuration
         dev = torch.device("cuda", local_rank % torch.cuda.device_count())
         torch.cuda.set_device(dev)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, init_method=init_method)
     else:
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, init_method=init_method)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     import distributed_training_amd as D
