@@ -586,6 +586,8 @@ class DistributedDataParallel(nn.Module):
         self._finalize_queued = False
         self._pending = {}
         self._record_order = not self._has_rebuilt_buckets and (self.static_graph or not self.find_unused_parameters)
+        if self.find_unused_parameters:
+            self._used_local = [0] * len(self._params)
         if self._record_order:
             self._ready_order = []
 
@@ -612,6 +614,8 @@ class DistributedDataParallel(nn.Module):
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
             if self._record_order:
                 self._ready_order.append(idx)
+            if self.find_unused_parameters:
+                self._used_local[idx] = 1
             g = param.grad
             ps = param.stride()
             # fast path: the grad has the strides of a parameter already seen to be dense
@@ -682,6 +686,8 @@ class DistributedDataParallel(nn.Module):
             # bucketer has unpacked them at finalize — step every bucket then
             self._overlap_step(range(len(b.buckets)))
         self._found_inf_valid = self._found_inf_target is not None
+        if self.find_unused_parameters and self.world_size > 1:
+            self._grads_of_locally_unused()
         if self.gradient_as_bucket_view:
             for i, p in enumerate(self._params):
                 if p.grad is not None:
@@ -691,6 +697,28 @@ class DistributedDataParallel(nn.Module):
         self._in_backward = False
         self._finalize_queued = False
         self._num_iterations += 1
+
+    def _grads_of_locally_unused(self):
+        """find_unused_parameters: a parameter unused on this rank but used on
+        another gets the averaged grad from its bucket, as torch's
+        ``copy_bucket_to_grad`` creates it (T:.../reducer.cpp finalize_bucket_dense:
+        ``global_unused`` from the all-reduced local-used map; globally unused
+        parameters keep their grad untouched).  One MAX all-reduce of the used
+        map per iteration and a host read of it — torch's Reducer does the same."""
+        used = torch.tensor(self._used_local, dtype=torch.int32)
+        if self._comm is not None:
+            used = used.to(self.device)
+            self._comm.all_reduce(used, op="max", stream=L.stream_ptr(self.device))
+        else:
+            if self._backend == "nccl":
+                used = used.to(self.device)
+            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=self.process_group)
+        glob = used.tolist()
+        b = self._bucketer
+        for i, p in enumerate(self._params):
+            if glob[i] and not self._used_local[i]:
+                view = b.bucket_view(i)
+                p.grad = view if self.gradient_as_bucket_view else view.clone(memory_format=torch.preserve_format)
 
     def _maybe_rebuild_buckets(self):
         if self._has_rebuilt_buckets or not (self.static_graph or not self.find_unused_parameters):

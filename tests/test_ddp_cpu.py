@@ -246,3 +246,55 @@ def _frozen(rank, ws):
 
 def test_frozen_parameters_broadcast_and_grads_match_torch():
     _run(_frozen, 2)
+
+
+class _Branchy(torch.nn.Module):
+    """`extra` is used on rank 0 only; `dead` on no rank."""
+
+    def __init__(self):
+        super().__init__()
+        self.body = _micro()
+        self.extra = torch.nn.Linear(10, 10)
+        self.dead = torch.nn.Linear(10, 10)
+
+    def forward(self, x, use_extra):
+        h = self.body(x)
+        return self.extra(h) if use_extra else h
+
+
+def _unused_across_ranks(rank, ws):
+    """find_unused_parameters with a parameter unused on one rank but used on
+    another: torch's Reducer gives that rank the averaged grad (it creates the
+    grad from the bucket); a parameter unused everywhere keeps grad None.
+    Three iterations, grads bit-identical to torch DDP's on every rank."""
+    import distributed_training_amd as D
+
+    out = {}
+    for impl in ("torch", "libgsync"):
+        torch.manual_seed(0)
+        model = _Branchy()
+        kw = dict(find_unused_parameters=True)
+        ddp = torch.nn.parallel.DistributedDataParallel(model, **kw) if impl == "torch" else \
+            D.DistributedDataParallel(model, **kw)
+        g = torch.Generator().manual_seed(1234 + rank)
+        grads = []
+        for _ in range(3):
+            for p in model.parameters():
+                p.grad = None
+            x = torch.rand(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            torch.nn.functional.cross_entropy(ddp(x, rank == 0), y).backward()
+            grads.append([None if p.grad is None else p.grad.clone() for p in model.parameters()])
+        out[impl] = grads
+    for it, (a, b) in enumerate(zip(out["torch"], out["libgsync"])):
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert (u is None) == (v is None), f"iter {it} param {i}: torch {u is None} libgsync {v is None}"
+            assert u is None or torch.equal(u, v), f"iter {it} param {i}"
+    names = [n for n, _ in _Branchy().named_parameters()]
+    last = out["libgsync"][-1]
+    assert all(last[i] is None for i, n in enumerate(names) if n.startswith("dead."))
+    assert all(last[i] is not None for i, n in enumerate(names) if n.startswith("extra."))
+
+
+def test_find_unused_parameters_used_on_another_rank():
+    _run(_unused_across_ranks, 2)
