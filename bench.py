@@ -405,12 +405,18 @@ def main():
             opt.zero_grad(set_to_none=True)
         return loss
 
+    skip_flags = []  # colossal engine: per-step GradScaler found-inf flags (device copies, no sync)
+
     def colossal_step(xb, yb):  # R:resnet/colossal/colossal_train.py:97-102
         loss = ccrit(cmodel(xb), yb)
         booster.backward(loss, opt_w)
         opt_w.step()
+        if record_skips[0]:
+            skip_flags.append(opt_w.scaler._state(opt_w.optim)["found_inf"].clone())
         opt_w.zero_grad()
         return loss
+
+    record_skips = [False]
 
     def torch_colossal_step(xb, yb):  # the same step on torch's own DDP / GradScaler / fused AdamW
         with torch.autocast("cuda", dtype=torch.float16):
@@ -452,11 +458,13 @@ def main():
         opt.enable_kernel_timer(args.steps + 4)
     else:
         zero.plan.timer_enable(4 * args.steps + 8)  # + the Σg² launches of the clip
+    record_skips[0] = args.engine == "colossal" and args.impl == "libgsync"
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    record_skips[0] = False
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -534,7 +542,13 @@ def main():
     elif zero is None:
         # update-kernel launches, HIP events recorded by libgsync on the launch stream
         # right around each kernel (the pointer-table upload, if any, stays outside)
-        opt_ms = sorted(opt_ms_saved)
+        opt_ms = opt_ms_saved
+        if skip_flags and len(skip_flags) == len(opt_ms):
+            # fp16 GradScaler: an overflowing step's update kernel exits at once on the
+            # device flag; only the launches that updated count toward the rate
+            skipped = [f.item() != 0 for f in skip_flags]
+            opt_ms = [ms for ms, sk in zip(opt_ms, skipped) if not sk]
+        opt_ms = sorted(opt_ms)
     else:
         # the fused shard update alone (plan launch timer); the whole zero.step() window
         # (norm, clip, update, all-gather) is reported beside it
@@ -687,6 +701,7 @@ def main():
                        + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
                           if args.optimizer_overlap else "")),
             "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
+            **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
             **({"rocprof": trace_check} if trace_check else {}),
         },
         "grad_sync": grad_sync,

