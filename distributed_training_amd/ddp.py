@@ -370,6 +370,10 @@ class DistributedDataParallel(nn.Module):
         self._pending: dict[int, Any] = {}
         self._num_iterations = 0
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
+        # find_unused_parameters: torch's local-used map — a parameter counts as used if its
+        # grad was produced in any backward since the last synchronising one (no_sync included)
+        self._used_local = [0] * len(self._params) if find_unused_parameters else None
+        self._ready_now: list = []
         self._overlap: dict | None = None  # _register_fused_optim state
         self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                               for i, p in enumerate(self._params)]
@@ -586,8 +590,7 @@ class DistributedDataParallel(nn.Module):
         self._finalize_queued = False
         self._pending = {}
         self._record_order = not self._has_rebuilt_buckets and (self.static_graph or not self.find_unused_parameters)
-        if self.find_unused_parameters:
-            self._used_local = [0] * len(self._params)
+        self._ready_now = []
         if self._record_order:
             self._ready_order = []
 
@@ -607,6 +610,8 @@ class DistributedDataParallel(nn.Module):
 
         def hook(param):
             if not self._in_backward:
+                if self._used_local is not None:
+                    self._used_local[idx] = 1  # a no_sync backward: used for the next sync
                 return
             if not self._finalize_queued:
                 self._finalize_queued = True
@@ -614,8 +619,9 @@ class DistributedDataParallel(nn.Module):
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
             if self._record_order:
                 self._ready_order.append(idx)
-            if self.find_unused_parameters:
+            if self._used_local is not None:
                 self._used_local[idx] = 1
+                self._ready_now.append(idx)
             g = param.grad
             ps = param.stride()
             # fast path: the grad has the strides of a parameter already seen to be dense
@@ -661,14 +667,24 @@ class DistributedDataParallel(nn.Module):
     def _finalize_backward(self):
         b = self._bucketer
         if self.find_unused_parameters:
+            # a parameter unused in this backward that still holds a grad (accumulated
+            # under no_sync) contributes that grad, as torch's mark_variable_ready_dense
+            # copies a defined grad of an unused variable into its bucket; the rest
+            # contribute zeros
+            fired = set(self._ready_now)
+            for i, p in enumerate(self._params):
+                if i not in fired and p.grad is not None:
+                    g = p.grad
+                    if not dense_like_param(g, p):
+                        dense = torch.empty_like(p)
+                        dense.copy_(g)
+                        p.grad = g = dense
+                    L.check(L.lib().gs_bucketer_mark_ready(b.handle, i, g.data_ptr(), self._stream, b._ready,
+                                                           ctypes.byref(b._n_ready)), "gs_bucketer_mark_ready")
+                    self._dispatch_ready(b)
             L.check(L.lib().gs_bucketer_mark_unused(b.handle, self._stream, b._ready, ctypes.byref(b._n_ready)),
                     "gs_bucketer_mark_unused")
-            if b._n_ready.value:
-                ready = [b._ready[k] for k in range(b._n_ready.value)]
-                if not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
-                    self._launch_external(ready)
-                elif self._overlap is not None:
-                    self._overlap_step(ready)
+            self._dispatch_ready(b)
         for bi in sorted(self._pending):
             kind, obj = self._pending[bi]
             if kind == "work":
@@ -686,8 +702,10 @@ class DistributedDataParallel(nn.Module):
             # bucketer has unpacked them at finalize — step every bucket then
             self._overlap_step(range(len(b.buckets)))
         self._found_inf_valid = self._found_inf_target is not None
-        if self.find_unused_parameters and self.world_size > 1:
-            self._grads_of_locally_unused()
+        if self.find_unused_parameters:
+            if self.world_size > 1:
+                self._grads_of_locally_unused()
+            self._used_local = [0] * len(self._params)  # torch resets the map after each sync
         if self.gradient_as_bucket_view:
             for i, p in enumerate(self._params):
                 if p.grad is not None:
@@ -697,6 +715,14 @@ class DistributedDataParallel(nn.Module):
         self._in_backward = False
         self._finalize_queued = False
         self._num_iterations += 1
+
+    def _dispatch_ready(self, b):
+        if b._n_ready.value:
+            ready = [b._ready[k] for k in range(b._n_ready.value)]
+            if not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
+                self._launch_external(ready)
+            elif self._overlap is not None:
+                self._overlap_step(ready)
 
     def _grads_of_locally_unused(self):
         """find_unused_parameters: a parameter unused on this rank but used on

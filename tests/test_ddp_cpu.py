@@ -298,3 +298,43 @@ def _unused_across_ranks(rank, ws):
 
 def test_find_unused_parameters_used_on_another_rank():
     _run(_unused_across_ranks, 2)
+
+
+def _unused_after_no_sync(rank, ws):
+    """find_unused_parameters + no_sync: a parameter used only in an
+    accumulation (no_sync) backward on one rank counts as used for the next
+    synchronising backward, and its accumulated grad is what it contributes
+    there (torch's local-used map spans the no_sync steps; an unused variable
+    with a defined grad is copied into its bucket).  Grads bit-identical to
+    torch DDP on both ranks, two rounds."""
+    import distributed_training_amd as D
+
+    out = {}
+    for impl in ("torch", "libgsync"):
+        torch.manual_seed(0)
+        m = _Branchy()
+        kw = dict(find_unused_parameters=True)
+        ddp = torch.nn.parallel.DistributedDataParallel(m, **kw) if impl == "torch" else \
+            D.DistributedDataParallel(m, **kw)
+        g = torch.Generator().manual_seed(1234 + rank)
+        res = []
+        for _ in range(2):
+            for p in m.parameters():
+                p.grad = None
+            with ddp.no_sync():
+                x = torch.rand(4, 3, 32, 32, generator=g)
+                y = torch.randint(0, 10, (4,), generator=g)
+                torch.nn.functional.cross_entropy(ddp(x, rank == 1), y).backward()
+            x = torch.rand(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            torch.nn.functional.cross_entropy(ddp(x, False), y).backward()
+            res.append([None if p.grad is None else p.grad.clone() for p in m.parameters()])
+        out[impl] = res
+    for it, (a, b) in enumerate(zip(out["torch"], out["libgsync"])):
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert (u is None) == (v is None), f"iter {it} param {i}"
+            assert u is None or torch.equal(u, v), f"iter {it} param {i}"
+
+
+def test_find_unused_parameters_used_under_no_sync():
+    _run(_unused_after_no_sync, 2)
