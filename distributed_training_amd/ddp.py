@@ -685,6 +685,13 @@ class DistributedDataParallel(nn.Module):
             L.check(L.lib().gs_bucketer_mark_unused(b.handle, self._stream, b._ready, ctypes.byref(b._n_ready)),
                     "gs_bucketer_mark_unused")
             self._dispatch_ready(b)
+        elif self.static_graph:
+            # static_graph: parameters the (fixed) graph never uses are marked ready at
+            # the end of backward, as torch's static-graph Reducer does; their slots
+            # reduce as zeros and, unused on every rank, their grads stay None
+            L.check(L.lib().gs_bucketer_mark_unused(b.handle, self._stream, b._ready, ctypes.byref(b._n_ready)),
+                    "gs_bucketer_mark_unused")
+            self._dispatch_ready(b)
         for bi in sorted(self._pending):
             kind, obj = self._pending[bi]
             if kind == "work":

@@ -338,3 +338,35 @@ def _unused_after_no_sync(rank, ws):
 
 def test_find_unused_parameters_used_under_no_sync():
     _run(_unused_after_no_sync, 2)
+
+
+def _static_graph_dead_layer(rank, ws):
+    """static_graph=True with a parameter the graph never uses: torch's
+    static-graph Reducer marks it ready at the end of backward (grad stays None);
+    libgsync did not and raised at finalize.  Three iterations, grads
+    bit-identical to torch DDP."""
+    import distributed_training_amd as D
+
+    out = {}
+    for impl in ("torch", "libgsync"):
+        torch.manual_seed(0)
+        m = _Branchy()
+        ddp = torch.nn.parallel.DistributedDataParallel(m, static_graph=True) if impl == "torch" else \
+            D.DistributedDataParallel(m, static_graph=True)
+        g = torch.Generator().manual_seed(1234 + rank)
+        res = []
+        for _ in range(3):
+            for p in m.parameters():
+                p.grad = None
+            x = torch.rand(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            torch.nn.functional.cross_entropy(ddp(x, True), y).backward()
+            res.append([None if p.grad is None else p.grad.clone() for p in m.parameters()])
+        out[impl] = res
+    for it, (a, b) in enumerate(zip(out["torch"], out["libgsync"])):
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert (u is None) == (v is None) and (u is None or torch.equal(u, v)), f"iter {it} param {i}"
+
+
+def test_static_graph_with_a_never_used_parameter():
+    _run(_static_graph_dead_layer, 2)
