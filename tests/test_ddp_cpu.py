@@ -370,3 +370,43 @@ def _static_graph_dead_layer(rank, ws):
 
 def test_static_graph_with_a_never_used_parameter():
     _run(_static_graph_dead_layer, 2)
+
+
+def _torch_hooks(rank, ws):
+    """torch's own comm hooks registered on libgsync DDP give torch DDP's grads
+    bit for bit: fp16_compress_hook, and the stateful PowerSGD hook (rank-1
+    compression after 2 plain iterations, error feedback, warm start) that
+    reads GradBucket.index / buffer / gradients / parameters / is_last."""
+    import distributed_training_amd as D
+    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks as dh
+    from torch.distributed.algorithms.ddp_comm_hooks import powerSGD_hook as ps
+
+    cases = {"fp16": lambda: (None, dh.fp16_compress_hook),
+             "powerSGD": lambda: (ps.PowerSGDState(process_group=None, matrix_approximation_rank=1,
+                                                   start_powerSGD_iter=2, min_compression_rate=0.5,
+                                                   use_error_feedback=True, warm_start=True, random_seed=0),
+                                  ps.powerSGD_hook)}
+    for name, make in cases.items():
+        out = {}
+        for impl in ("torch", "libgsync"):
+            torch.manual_seed(0)
+            m = _micro()
+            ddp = torch.nn.parallel.DistributedDataParallel(m) if impl == "torch" else D.DistributedDataParallel(m)
+            ddp.register_comm_hook(*make())
+            g = torch.Generator().manual_seed(1234 + rank)
+            res = []
+            for _ in range(4):
+                for p in m.parameters():
+                    p.grad = None
+                x = torch.rand(4, 3, 32, 32, generator=g)
+                y = torch.randint(0, 10, (4,), generator=g)
+                torch.nn.functional.cross_entropy(ddp(x), y).backward()
+                res.append([p.grad.clone() for p in m.parameters()])
+            out[impl] = res
+        for it, (a, b) in enumerate(zip(out["torch"], out["libgsync"])):
+            for i, (u, v) in enumerate(zip(a, b)):
+                assert torch.equal(u, v), f"{name} iter {it} param {i}"
+
+
+def test_torch_comm_hooks_fp16_and_powersgd_match_torch():
+    _run(_torch_hooks, 2)
