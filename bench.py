@@ -243,6 +243,10 @@ class _OverlappedStep:
 
 def main():
     args = parse()
+    if os.environ.get("GSYNC_BENCH_TRACEBACK_S"):  # debugging aid: every rank's stacks every N s
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["GSYNC_BENCH_TRACEBACK_S"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
