@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--optimizer-overlap", type=int, default=0,
                     help="1: DDP._register_fused_optim — each bucket's fused update runs behind its unpack "
                          "under backward (torch's overlapped-optimizer API); no optimizer.step() after backward")
+    ap.add_argument("--policy-ab", type=int, default=-1,
+                    help="after the timed region: re-wrap the model with each DDP bucket policy (torch, xgmi, "
+                         "last-bucket cap 1 MiB, torch again) and time each, with tail, bus bandwidth and parity "
+                         "(-1: only at N > 1 on the DDP engine) — the data for DESIGN §8's policy rule")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -125,7 +129,7 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
                         lambda f=flat, s=shard: comm.all_gather(s, f)))
     out = []
     torch.cuda.synchronize()
-    dist.barrier()
+    _BenchColl(comm, comm.device, "nccl").barrier()
     with torch.cuda.stream(comm.stream):
         for kind, nbytes, fn in ops:
             for _ in range(warmup):
@@ -213,6 +217,130 @@ def grad_sync_kernel_rates(params, dev, iters=20):
                       f"{iters} launches", "min_frac": min(r["frac"] for r in rows.values())}
 
 
+class _BenchColl:
+    """The bench's own barriers and MAX-over-ranks: on the engine's libgsync
+    communicator when it has one (one RCCL communicator per rank), else on the
+    process group."""
+
+    def __init__(self, comm, dev, pg_backend):
+        self.comm = comm
+        self.dev = dev
+        self.pg_backend = pg_backend
+
+    def barrier(self):
+        if self.comm is not None:
+            t = torch.zeros(1, device=self.dev)
+            self.comm.all_reduce(t, stream=torch.cuda.current_stream(self.dev).cuda_stream)
+            torch.cuda.synchronize(self.dev)
+        else:
+            dist.barrier()
+
+    def max(self, x: float) -> float:
+        on_dev = self.comm is not None or self.pg_backend == "nccl"
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev if on_dev else "cpu")
+        if self.comm is not None:
+            self.comm.all_reduce(t, op="max", stream=torch.cuda.current_stream(self.dev).cuda_stream)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def _engine_comm(ddp, zero):
+    if zero is not None:
+        return zero._comm
+    for m in (ddp, getattr(ddp, "module", None)):
+        c = getattr(m, "_comm", None)
+        if c is not None:
+            return c
+    return None
+
+
+# DESIGN §8 decision rule for the bucket policy (row N1), fixed before the
+# driver's N > 1 run: a variant replaces the torch layout as the default when
+# its images/s beat the mean of the two torch-layout runs (before and after,
+# to cancel drift) by >= 0.5 % with parity.ok; the best such variant wins.
+POLICY_MARGIN = 0.005
+
+
+def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
+    """Re-wrap `model` with each bucket policy and time `steps` steps of each
+    (after a one-bucket first step and the rebuild step), rank-synchronised
+    and MAX over ranks like the headline; per variant: images/s, the exposed
+    tail (timed steps) and its split, in-step and standalone all-reduce bus
+    bandwidth against (n-1) x 153 GB/s, and the self-checked parity step."""
+    import distributed_training_amd as D
+    from distributed_training_amd import parity as PC
+
+    variants = [("torch", {}), ("xgmi", {"bucket_policy": "xgmi"}),
+                ("last_bucket_cap_1MiB", {"last_bucket_cap_mb": 1.0}), ("torch_again", {})]
+    bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
+    ddp.close()
+    peak = (world - 1) * XGMI_LINK_GBPS
+    rows = {}
+    for name, kw in variants:
+        v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
+                                      gradient_as_bucket_view=args.grad_as_bucket_view, **kw)
+
+        def fwd_bwd():
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = crit(v(x), y)
+            loss.backward()
+
+        def one():
+            fwd_bwd()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+
+        for _ in range(2):
+            one()
+        torch.cuda.synchronize()
+        c = _BenchColl(v._comm, dev, args.pg_backend)
+        c.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        c.barrier()
+        el = c.max(time.perf_counter() - t0)
+        tail_timed = v.tail_ms()
+        v.set_timeline(2)
+        one()
+        torch.cuda.synchronize()
+        comm_ms = [m for m in v.bucket_comm_ms() if m >= 0]
+        tail = v.tail_ms()
+        v.set_timeline(1)
+        bucket_bytes = [b.numel() * b.element_size() for b in v._bucketer.buffers]
+        row = {"images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3,
+               "bucket_bytes": bucket_bytes, "tail_ms_timed": tail_timed["total"] if tail_timed else None,
+               "tail_split_ms": tail}
+        if world > 1 and comm_ms and min(comm_ms) > 0:
+            bus = sum(bucket_bytes) / (sum(comm_ms) * 1e-3) * 2 * (world - 1) / world / 1e9
+            row["in_step_bus_GBps"] = bus
+            row["in_step_frac"] = bus / peak
+        if v._comm is not None and world > 1:
+            sa = collective_bench(v, None, world)
+            row["standalone"] = {"bus_GBps": sa["bus_GBps"], "frac": sa["frac"], "ms_per_step": sa["ms_per_step"],
+                                 "whole_grad": next((r for r in sa["per_op"] if r["op"] == "all_reduce_whole_grad"),
+                                                    None)}
+        cal = v._get_ddp_logging_data().get("xgmi_calibration")
+        if cal:
+            row["xgmi_calibration"] = cal
+        row["parity"] = PC.ddp_parity_step(v, opt, fwd_bwd)
+        rows[name] = row
+        v.close()
+    base = (rows["torch"]["images_per_sec"] + rows["torch_again"]["images_per_sec"]) / 2
+    best, best_ips = "torch", base * (1 + POLICY_MARGIN)
+    for name in ("xgmi", "last_bucket_cap_1MiB"):
+        r = rows[name]
+        r["vs_torch"] = r["images_per_sec"] / base
+        if r["parity"] and r["parity"].get("ok") and r["images_per_sec"] >= best_ips:
+            best, best_ips = name, r["images_per_sec"]
+    return {"variants": rows, "steps_each": steps, "torch_mean_images_per_sec": base,
+            "rule": f"a variant becomes the default if images/s >= (1 + {POLICY_MARGIN}) x the mean of the two "
+                    "torch-layout runs with parity.ok (DESIGN §8); best such variant wins",
+            "decision": best}
+
+
 class _OverlappedStep:
     """The bench's optimizer handle under --optimizer-overlap: the update already
     ran per bucket inside backward, so step() is empty; kernel_ms() is the sum
@@ -273,7 +401,12 @@ def main():
     else:
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, init_method=init_method)
+        # libgsync brings up its own RCCL communicator (unique id through the store) and
+        # the bench's barriers / MAX go through it (_BenchColl): no device_id, so torch's
+        # ProcessGroupNCCL never builds a second communicator on the rank; --impl torch
+        # uses the process group itself (eager init)
+        kw = dict(device_id=dev) if args.impl == "torch" else {}
+        dist.init_process_group("nccl", rank=rank, world_size=world, init_method=init_method, **kw)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     import distributed_training_amd as D
@@ -463,18 +596,16 @@ def main():
     else:
         zero.plan.timer_enable(4 * args.steps + 8)  # + the Σg² launches of the clip
     record_skips[0] = args.engine == "colossal" and args.impl == "libgsync"
-    dist.barrier()
+    coll_h = _BenchColl(_engine_comm(ddp, zero) if args.impl == "libgsync" else None, dev, args.pg_backend)
+    coll_h.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
     record_skips[0] = False
     torch.cuda.synchronize()
-    dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.pg_backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+    coll_h.barrier()
+    elapsed = coll_h.max(time.perf_counter() - t0)
     # the timed launches' kernel durations, read before any untimed step below adds more
     opt_ms_saved = zero_ms_saved = None
     if args.impl == "libgsync" and not args.graph:
@@ -532,6 +663,15 @@ def main():
             parity = PC.zero_parity_step(zero, fwd_bwd)
         if rank == 0:
             print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
+
+    policy_ab = None
+    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
+    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
+            and not args.optimizer_overlap):
+        # after every reading of the headline DDP above: it is closed here
+        policy_ab = bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args)
+        if rank == 0:
+            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
 
     if args.impl == "torch":
         opt_ms = []
@@ -711,6 +851,7 @@ def main():
         "grad_sync": grad_sync,
         "grad_sync_kernels": kernel_rates,
         "parity": parity,
+        **({"bucket_policy_ab": policy_ab} if policy_ab is not None else {}),
         **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
         "warmup_s": warm_s,
         "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,

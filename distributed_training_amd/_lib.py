@@ -96,6 +96,8 @@ SIGNATURES = {
     "gs_scale": (_c_int, [_vp, _c_int, _c_int, _c_f, _c_int, _vp]),
     "gs_sqnorm": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_sum": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
+    "gs_sqnorm_partial": (_c_int, [_vp, _c_int, _c_int, _vp]),
+    "gs_plan_set_clip": (_c_int, [_vp, _vp, _c_f, _c_f, _c_f, _c_f, _vp]),
     "gs_rng_state_bytes": (_c_int, []),
     "gs_rng_draw_u32": (_c_int, [_vp, _c_i64, _c_i64, _vp]),
     "gs_randperm": (_c_int, [ctypes.c_uint64, _c_i64, _vp]),

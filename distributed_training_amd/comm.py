@@ -4,8 +4,9 @@ The unique id is created on rank 0 and handed to the other ranks through the
 caller's ``torch.distributed`` process group (the same rendezvous the
 reference uses: ``init_process_group`` at R:resnet/pytorch_ddp/ddp_train.py:84),
 after which all gradient traffic goes through this communicator on its own
-high-priority stream — torch's ProcessGroupNCCL is only used for the
-bootstrap.
+high-priority stream.  The id travels through the rendezvous store, not a
+process-group collective, so torch's ProcessGroupNCCL never has to bring up a
+second RCCL communicator on the rank.
 """
 from __future__ import annotations
 
@@ -38,10 +39,7 @@ class Communicator:
         uid = (ctypes.c_uint8 * nbytes)()
         if self.rank == 0:
             L.check(lib.gs_comm_get_unique_id(uid), "gs_comm_get_unique_id")
-        obj = [bytes(uid)]
-        group_src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
-        dist.broadcast_object_list(obj, src=group_src, group=process_group, device=self._bootstrap_device())
-        uid = (ctypes.c_uint8 * nbytes).from_buffer_copy(obj[0])
+        uid = (ctypes.c_uint8 * nbytes).from_buffer_copy(self._exchange_uid(bytes(uid)))
         h = ctypes.c_void_p()
         torch.cuda.set_device(device)
         L.check(lib.gs_comm_create(self.rank, self.world, uid, device.index, ctypes.byref(h)), "gs_comm_create")
@@ -71,9 +69,32 @@ class Communicator:
         if aborted:
             raise L.GsyncError(f"libgsync communicator (rank {self.rank}/{self.world}) aborted: {why}")
 
-    def _bootstrap_device(self):
-        backend = dist.get_backend(self.pg)
-        return self.device if backend in ("nccl", "rccl") else torch.device("cpu")
+    def _exchange_uid(self, uid: bytes) -> bytes:
+        """Rank 0's RCCL unique id to every rank through the rendezvous store
+        (the TCP store torch.distributed.init_process_group already holds) —
+        not a collective on the process group: with the nccl backend that would
+        bring up torch's own RCCL communicator beside this one (two sets of
+        channels and proxy threads per rank).  Keys are namespaced by group
+        and by creation count, which every rank advances in the same order."""
+        store = None
+        try:
+            store = dist.distributed_c10d._get_default_store()
+        except Exception:  # pragma: no cover - a torch without the private accessor
+            store = None
+        if store is None:
+            obj = [uid]
+            src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+            backend = dist.get_backend(self.pg)
+            dev = self.device if backend in ("nccl", "rccl") else torch.device("cpu")
+            dist.broadcast_object_list(obj, src=src, group=self.pg, device=dev)
+            return obj[0]
+        name = getattr(self.pg if self.pg is not None else dist.group.WORLD, "group_name", "world")
+        gen = _UID_GEN[name] = _UID_GEN.get(name, -1) + 1
+        key = f"gsync/uid/{name}/{gen}"
+        if self.rank == 0:
+            store.set(key, uid)
+            return uid
+        return bytes(store.get(key))
 
     def close(self):
         h = getattr(self, "handle", None)
@@ -127,6 +148,7 @@ class Communicator:
 
 
 _COMMS: dict = {}
+_UID_GEN: dict = {}  # group name -> communicators created for it so far (store key namespace)
 
 
 def get_communicator(process_group=None, device=None) -> Communicator:

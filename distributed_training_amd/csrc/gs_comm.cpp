@@ -32,8 +32,12 @@ struct gs_comm {
   hipStream_t stream = nullptr;
   int rank = 0, world = 1, device = 0;
   std::atomic<bool> aborted{false};
-  std::string abort_reason;
+  std::string abort_reason;  // written once, by the winner of `aborted`, under reason_mu
+  std::mutex reason_mu;
   std::mutex mu;  // enqueue (comm_enqueue) vs abort vs the watchdog's bookkeeping
+  // steady-clock ns at which the enqueue now holding `mu` started (0: none):
+  // the watchdog times a blocked enqueue from here, not from when it noticed
+  std::atomic<int64_t> enq_since{0};
   // watchdog
   int64_t timeout_ms = 0;
   std::thread wd;
@@ -96,12 +100,27 @@ int to_nccl_op(int op, ncclRedOp_t* out) {
 // collective (a pack, a fill).  gs_comm_stream() hands out the comm stream.
 hipStream_t pick(gs_comm*, void* stream) { return static_cast<hipStream_t>(stream); }
 
-// caller holds c->mu
+// First caller wins (compare-exchange on `aborted`), so the reason is written
+// once even when the watchdog aborts a blocked enqueue without c->mu; every
+// other caller holds c->mu.
 void abort_locked(gs_comm* c, const std::string& why) {
-  if (c->aborted.load()) return;
-  c->abort_reason = why;
-  c->aborted.store(true);
+  {
+    std::lock_guard<std::mutex> lk(c->reason_mu);
+    bool expected = false;
+    if (!c->aborted.compare_exchange_strong(expected, true)) return;
+    c->abort_reason = why;
+  }
   if (c->comm) (void)ncclCommAbort(c->comm);
+}
+
+std::string abort_reason(gs_comm* c) {
+  std::lock_guard<std::mutex> lk(c->reason_mu);
+  return c->abort_reason;
+}
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // > 0 while a graph capture is being recorded (gs_watchdog_pause): event
@@ -111,24 +130,26 @@ std::atomic<int> g_wd_pause{0};
 void watchdog_loop(gs_comm* c) {
   (void)hipSetDevice(c->device);
   using clk = std::chrono::steady_clock;
-  auto busy_since = clk::time_point();
   while (!c->wd_stop.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
     if (g_wd_pause.load() > 0) continue;
     // enqueues hold c->mu for the few microseconds of an RCCL enqueue, so the
     // abort never frees the communicator under a concurrent enqueue; only an
-    // enqueue that itself hangs (holding the lock past the timeout) is
-    // aborted without it — that enqueue is what the abort has to break
+    // enqueue that itself hangs (holding the lock past the timeout, measured
+    // from the enqueue's own start) is aborted without it — that enqueue is
+    // what the abort has to break.  A first collective that blocks in RCCL's
+    // lazy connection setup while a peer is late counts against the timeout
+    // too (as ProcessGroupNCCL's watchdog counts it): set the timeout above the
+    // slowest expected start-up.
     std::unique_lock<std::mutex> lk(c->mu, std::try_to_lock);
     if (!lk.owns_lock()) {
-      if (busy_since == clk::time_point()) busy_since = clk::now();
-      const auto held = std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - busy_since);
-      if (c->timeout_ms > 0 && held.count() > c->timeout_ms && !c->aborted.load())
-        abort_locked(c, "watchdog: an RCCL enqueue has been blocked for " + std::to_string(held.count()) +
+      const int64_t t0 = c->enq_since.load();
+      const int64_t held_ms = t0 ? (now_ns() - t0) / 1000000 : 0;
+      if (c->timeout_ms > 0 && held_ms > c->timeout_ms)
+        abort_locked(c, "watchdog: an RCCL enqueue has been blocked for " + std::to_string(held_ms) +
                             " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
       continue;
     }
-    busy_since = clk::time_point();
     if (c->aborted.load()) continue;
     ncclResult_t async = ncclSuccess;
     if (c->comm && ncclCommGetAsyncError(c->comm, &async) == ncclSuccess && async != ncclSuccess &&
@@ -182,8 +203,10 @@ int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_
   if (!c) return fail(GS_EINVAL, "no communicator");
   GsRange range(what);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (c->aborted.load()) return fail(GS_ERCCL, "communicator aborted: " + c->abort_reason);
+  if (c->aborted.load()) return fail(GS_ERCCL, "communicator aborted: " + abort_reason(c));
+  c->enq_since.store(now_ns());
   const ncclResult_t r = fn();
+  c->enq_since.store(0);
   if (r != ncclSuccess) return rccl_fail(r, what);
   return comm_track_locked(c, stream);
 }
@@ -284,7 +307,7 @@ int gs_comm_status(gs_comm* c, char* reason, int cap) {
       abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
   }
   if (reason && cap > 0) {
-    const std::string& r = c->abort_reason;
+    const std::string r = abort_reason(c);
     const size_t n = std::min(r.size(), static_cast<size_t>(cap - 1));
     std::memcpy(reason, r.data(), n);
     reason[n] = 0;

@@ -125,6 +125,7 @@ struct PlanArgs {
   float* red_out;             // fused reduction target (chunk engine), NULL = none
   int32_t red_acc;            // accumulate into red_out
   int32_t red_fuse;           // R > 0: combine in-kernel (two-level ticket, R groups), no combine launch
+  int32_t red_groups_only;    // stop after the group level: the R group sums stay for a clipped update
   int32_t per_wg;             // chunk engine: groups per workgroup (0 = grid-stride)
   int32_t n;
   int32_t n_tasks;
@@ -140,6 +141,20 @@ struct AdamHyper {
   float b2, w1, w2, eps, wd, step_size, bc2s, decay;  // w1 = float(1-b1), decay = float(1-lr*wd)
   int adamw, maximize;
 };
+// Gradient-norm clip folded into an update launch (gs_plan_set_clip): the
+// update's workgroups form the coefficient themselves, so no coefficient
+// launch (and, with the plan's own group sums, no combine launch) sits between
+// the Σg² kernel and the update.  Same arithmetic as the separate path
+// (sq *= gscale², sq *= sq_mul; norm = sqrt(sq); coef = min(1, max/(norm+eps))
+// * gscale * coef_mul, T:nn/utils/clip_grad.py:165-174), so it is bit-identical.
+struct ClipArgs {
+  const float* sq;     // a finished Σg² (groups == 0) or `groups` group sums, kRedSyncStride apart
+  int32_t groups;
+  float max_norm, eps;
+  float sq_mul, coef_mul;  // host multipliers (ZeRO's loss scale): 1 = none
+  float* out;          // [sq, coef, norm] written by workgroup 0 (nullable)
+};
+
 inline SgdHyper make_sgd(double lr, double mom, double damp, double wd, int nest, int maxi,
                          int first) {
   return SgdHyper{static_cast<float>(lr), static_cast<float>(mom),
@@ -187,6 +202,13 @@ struct gs_plan {
   unsigned long long table_capture_id = 0;  // capture that last recorded a table write
   bool in_graph = false;        // a graph holds a table write: re-upload before eager launches
   const float* hyper = nullptr; // device hyper-parameter source of sgd/adam (gs_plan_set_hyper_source)
+  // clip folded into sgd/adam (gs_plan_set_clip); clip_own: Σg² from this plan's
+  // group sums, left by its last gs_sqnorm_partial (red_groups of them)
+  bool clip_on = false, clip_own = false;
+  gs::ClipArgs clip{};
+  int red_groups = 0;
+  bool red_valid = false;       // a gs_sqnorm_partial has run on this plan
+  float h_red = 0.f;            // host plans: the Σg² of gs_sqnorm_partial
   // launch timer ring (gs_plan_timer_enable)
   std::vector<void*> timer_ev;  // [2 * slots]: start, stop
   std::vector<int32_t> timer_kind;  // [slots]: GS_OP_* of the timed launch
@@ -261,10 +283,13 @@ int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float
                   void* stream);
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
                       void* stream);
+int hip_sqnorm_partial(gs_plan* p, int slot, int dt, void* stream);
+const float* hip_plan_red_groups(const gs_plan* p);  // the 64 group sums of gs_sqnorm_partial
+float* hip_plan_red_scalar(const gs_plan* p);        // its finished Σ when red_groups == 0
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi,
-            void* stream);
+            const ClipArgs* clip, void* stream);
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs, const float* fi,
-             void* stream);
+             const ClipArgs* clip, void* stream);
 int hip_device_count();
 int hip_memset_async(void* dst, int value, size_t bytes, void* stream);
 int hip_stream_wait(void* waiter, void* signaler);
@@ -279,6 +304,10 @@ int host_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc);
 int host_sum(gs_plan* p, int slot, int dt, float* out, int acc);
 int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm);
 int host_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found);
-int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi);
-int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs, const float* fi);
+int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi,
+             const ClipArgs* clip);
+int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs, const float* fi,
+              const ClipArgs* clip);
+// the clip coefficient of ClipArgs on the host (groups == 0: *sq is final)
+float host_clip_factor(const ClipArgs& c, const float* gs);
 }  // namespace gs

@@ -256,13 +256,33 @@ int host_unscale_check(gs_plan* p, int s_, int dt, const float* inv, float* foun
   return GS_OK;
 }
 
-int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi) {
+float host_clip_factor(const ClipArgs& c, const float* gsc) {
+  float sq = c.sq[0];
+  const float s = gsc ? gsc[0] : 1.f;
+  if (gsc) sq = sq * (s * s);
+  sq = sq * c.sq_mul;
+  const float nrm = std::sqrt(sq);
+  float coef = c.max_norm / (nrm + c.eps);
+  coef = coef < 1.f ? coef : 1.f;
+  if (gsc) coef = coef * s;
+  coef = coef * c.coef_mul;
+  if (c.out) {
+    c.out[0] = sq;
+    c.out[1] = coef;
+    c.out[2] = nrm;
+  }
+  return coef;
+}
+
+int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
+             const ClipArgs* clip) {
+  const float cf = clip ? host_clip_factor(*clip, gsc) : 1.f;  // published even on a skipped step
   if (fi && fi[0] != 0.f) {
     GS_TRY_RET(check_float(gdt));
     return GS_OK;
   }
-  const bool has_gs = gsc != nullptr;
-  const float gs = has_gs ? gsc[0] : 1.f;
+  const bool has_gs = gsc != nullptr || clip != nullptr;
+  const float gs = clip ? cf : (gsc ? gsc[0] : 1.f);
   GS_HOST_FLOAT(gdt, GD, GS_HOST_LOWP(ldt, LD, {
     for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
       float* pp = static_cast<float*>(slot(p, 0, t));
@@ -289,13 +309,14 @@ int host_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, 
 }
 
 int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc,
-              const float* fi) {
+              const float* fi, const ClipArgs* clip) {
+  const float cf = clip ? host_clip_factor(*clip, gsc) : 1.f;  // published even on a skipped step
   if (fi && fi[0] != 0.f) {
     GS_TRY_RET(check_float(gdt));
     return GS_OK;
   }
-  const bool has_gs = gsc != nullptr;
-  const float gs = has_gs ? gsc[0] : 1.f;
+  const bool has_gs = gsc != nullptr || clip != nullptr;
+  const float gs = clip ? cf : (gsc ? gsc[0] : 1.f);
   GS_HOST_FLOAT(gdt, GD, GS_HOST_LOWP(ldt, LD, {
     for_ranges(p, [&](int t, int64_t i0, int64_t i1) {
       float* pp = static_cast<float*>(slot(p, 0, t));

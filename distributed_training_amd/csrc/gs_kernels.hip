@@ -516,8 +516,8 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op 
   __shared__ int64_t s_ubeg[kMaxSegPerTask];
   __shared__ int32_t s_pref[kMaxSegPerTask + 1];
   float acc = 0.f;
+  load_hyper(op);             // uniform: graph-replayable lr / bias corrections, clip coefficient
   if (!op.active()) return;  // uniform across the grid
-  load_hyper(op);             // uniform: graph-replayable lr / bias corrections
   for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
     const int sb = cload(P.task_begin, task);
     const int ns = cload(P.task_begin, task + 1) - sb;
@@ -690,8 +690,8 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   constexpr int G = Op::kG;
   static_assert(G == 1 || G == 2 || G == 4 || G == 8, "group of 1, 2, 4 or 8 chunks");
   float acc = 0.f;
+  load_hyper(op);            // uniform: graph-replayable lr / bias corrections, clip coefficient
   if (!op.active()) return;  // uniform across the grid
-  load_hyper(op);            // uniform: graph-replayable lr / bias corrections
   __shared__ int64_t s_lo[kMixedStage], s_hi[kMixedStage];  // mixed chunks: the span's extents
   __shared__ TV s_tv[kMixedStage];                            // ... and descriptors
   const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
@@ -772,9 +772,15 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
     if (threadIdx.x == 0) {
       __hip_atomic_store(&P.ticket[k * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&gsums[k * kStride], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t tk = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_role = tk == static_cast<uint32_t>(n_groups) - 1 ? 2 : 0;
+      if (P.red_groups_only) {
+        // gs_sqnorm_partial: the group sums are the result; the clipped update
+        // on this plan folds them (clip_multiplier), no top-level hand-off
+        s_role = 0;
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_role = tk == static_cast<uint32_t>(n_groups) - 1 ? 2 : 0;
+      }
     }
     __syncthreads();
     if (s_role != 2 || threadIdx.x >= 64) return;
@@ -1069,6 +1075,10 @@ struct SgdOp {
   const float* gscale;
   const float* found_inf;
   const float* hyper = nullptr;  // [lr] in device memory (gs_plan_set_hyper_source)
+  ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
+  bool clip_on = false;
+  bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
+  float gsv = 1.f;
   struct Frag { float p[N], g[N], b[N]; };
   __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
@@ -1083,11 +1093,10 @@ struct SgdOp {
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
-    const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       float g = f.g[i];
-      if (gscale) g = g * gs;                       // clip_grad_norm_ / unscale: grads *= coef
+      if (use_gs) g = g * gsv;                      // clip_grad_norm_ / unscale: grads *= coef
       if (h.maximize) g = -g;
       if (h.wd != 0.f) g = fmaf(h.wd, f.p[i], g);   // grad.add(param, alpha=wd)
       float d = g;
@@ -1118,6 +1127,10 @@ struct AdamOp {
   const float* gscale;
   const float* found_inf;
   const float* hyper = nullptr;  // [step_size, bc2_sqrt, 1 - lr*wd] in device memory
+  ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
+  bool clip_on = false;
+  bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
+  float gsv = 1.f;
   struct Frag { float p[N], g[N], m[N], v[N]; };
   __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
@@ -1133,11 +1146,10 @@ struct AdamOp {
   }
   template <bool F>
   __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {
-    const float gs = gscale ? *gscale : 1.f;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       float g = f.g[i];
-      if (gscale) g = g * gs;
+      if (use_gs) g = g * gsv;
       if (h.maximize) g = -g;
       float p = f.p[i];
       if (h.wd != 0.f) {
@@ -1157,12 +1169,48 @@ struct AdamOp {
   }
 };
 
+// The update's grad multiplier, formed once per workgroup (uniform): *gscale
+// (AMP unscale / a precomputed clip coefficient) or, with a folded clip, the
+// clip coefficient itself — from a finished Σg² or from the Σg² kernel's group
+// sums (lane j reads group j and the wave folds them: the fused combine's own
+// last step, so the result is bit-identical to gs_sqnorm's), then exactly
+// clip_coef_kernel's arithmetic.  Workgroup 0 publishes [Σg², coef, norm].
+__device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float* gscale) {
+  float sq;
+  if (c.groups > 0) {
+    const int l = static_cast<int>(threadIdx.x & 63);
+    const float x = l < c.groups ? c.sq[l * kRedSyncStride] : 0.f;
+    sq = wave_sum(0.f + x);
+  } else {
+    sq = c.sq[0];
+  }
+  const float s = gscale ? *gscale : 1.f;
+  if (gscale) sq = sq * (s * s);                    // the norm of the unscaled grads
+  sq = sq * c.sq_mul;
+  const float nrm = sqrtf(sq);
+  float coef = c.max_norm / (nrm + c.eps);
+  coef = coef < 1.f ? coef : 1.f;
+  if (gscale) coef = coef * s;
+  coef = coef * c.coef_mul;
+  if (c.out && blockIdx.x == 0 && threadIdx.x == 0) {
+    c.out[0] = sq;
+    c.out[1] = coef;
+    c.out[2] = nrm;
+  }
+  return coef;
+}
+template <class Op>
+__device__ __forceinline__ void load_grad_multiplier(Op& op) {
+  op.use_gs = op.gscale != nullptr || op.clip_on;
+  op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
+}
 template <int N, int GD, int LD>
 __device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD>& op) {
   if (op.hyper) {
     op.h.lr = op.hyper[0];
     if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
   }
+  load_grad_multiplier(op);
 }
 template <int N, int GD, int LD>
 __device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD>& op) {
@@ -1171,6 +1219,7 @@ __device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD>& op) {
     op.h.bc2s = op.hyper[1];
     op.h.decay = op.hyper[2];
   }
+  load_grad_multiplier(op);
 }
 
 __global__ void clip_coef_kernel(const float* sq, float max_norm, float eps, float* coef,
@@ -1198,8 +1247,11 @@ struct DeviceGuard {
   }
 };
 
+// groups_only (gs_sqnorm_partial): the fused reduction stops at its R group
+// sums, which stay in the plan for the next clipped update (p->red_groups)
 template <int ILP, class Op>
-int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0) {
+int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0,
+           int groups_only = 0) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->n == 0 || p->segs.empty()) {
     if (Op::kRed != 0 && red_out && !accumulate) HIP_RET(hipMemsetAsync(red_out, 0, 4, s));
@@ -1219,16 +1271,20 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   bool fused = false;
   if (chunk) {
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
-    const bool red = Op::kRed != 0 && red_out;
+    const bool red = Op::kRed != 0 && (red_out || groups_only);
     int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
-    fused = red && cap <= kRedFuseMaxGrid && red_fuse_groups() > 0;
+    fused = red && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
     if (fused) cap = std::min(cap, red_grid_cap(GS_RED_FUSE_GRID));
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     PlanArgs a = p->args();
     a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
     a.red_out = Op::kRed != 0 ? red_out : nullptr;
     a.red_acc = accumulate;
-    a.red_fuse = fused ? red_fuse_groups() : 0;
+    // groups-only: always the full 64 groups (kRedMaxGroups: one per lane of the
+    // update's fold), whatever GS_RED_FUSE says for the ordinary reductions
+    a.red_fuse = fused ? (groups_only ? kRedMaxGroups : red_fuse_groups()) : 0;
+    a.red_groups_only = groups_only;
+    if (groups_only) p->red_groups = std::min(grid, kRedMaxGroups);
     a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
     hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
   } else {
@@ -1316,7 +1372,9 @@ int hip_plan_upload_static(gs_plan* p) {
   HIP_RET(hipMemset(p->d_table, 0, tb));
   // per-workgroup partials + the fused reduction's counters / group sums (zeroed once;
   // every fused launch leaves them at zero)
-  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials), sizeof(float) * (kGridLimit + kRedSyncWords)));
+  // (+ one more line: the Σg² scalar of gs_sqnorm_partial when the chunk engine is off)
+  HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials),
+                    sizeof(float) * (kGridLimit + kRedSyncWords + kRedSyncStride)));
   HIP_RET(hipMemset(p->d_partials + kGridLimit, 0, sizeof(float) * kRedSyncWords));
   HIP_RET(hipHostMalloc(&p->pinned, tb * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) {
@@ -1542,6 +1600,29 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
   return GS_OK;
 }
 
+// Σ x² of one slot left in the plan for a clipped update (gs_sqnorm_partial):
+// the chunk kernel with the in-kernel combine stopped at its 64 group sums
+// (no combine launch, no top-level hand-off); the update's workgroups fold them
+// (clip_multiplier).  The task engine (GS_ENGINE A/B runs) or an empty plan
+// writes the finished Σ into the plan's scalar word instead (red_groups = 0).
+const float* hip_plan_red_groups(const gs_plan* p) {
+  return p->d_partials + kGridLimit + (kRedMaxGroups + 1) * kRedSyncStride;
+}
+float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit + kRedSyncWords; }
+
+int hip_sqnorm_partial(gs_plan* p, int slot, int dt, void* stream) {
+  DeviceGuard g(p->device);
+  const bool groups = use_chunk_engine(GS_OP_SQNORM) && !p->chunks.empty() && p->n > 0 && !p->segs.empty();
+  GS_DISPATCH_FLOAT(dt, DT, {
+    SqnormOp<GS_PACK_N, DT> op;
+    op.slot = slot;
+    if (groups) return launch<GS_RED_ILP>(p, op, stream, nullptr, 0, 1);
+    p->red_groups = 0;
+    return launch<GS_RED_ILP>(p, op, stream, hip_plan_red_scalar(p), 0);
+  });
+  return GS_OK;
+}
+
 int hip_sum(gs_plan* p, int slot, int dt, float* out, int acc, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
@@ -1586,22 +1667,24 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
 }
 
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
-            void* stream) {
+            const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     SgdOp<GS_OPT_N, GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
+    if (clip) { op.clip = *clip; op.clip_on = true; }
     return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;
 }
 
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
-             void* stream) {
+             const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
     AdamOp<GS_OPT_N, GD, LD> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
+    if (clip) { op.clip = *clip; op.clip_on = true; }
     return launch<GS_OPT_ILP>(p, op, stream);
   }));
   return GS_OK;

@@ -54,6 +54,7 @@ gs::PlanArgs gs_plan::args() const {
   a.red_out = nullptr;
   a.red_acc = 0;
   a.red_fuse = 0;
+  a.red_groups_only = 0;
   a.per_wg = 0;
   a.ptrs = static_cast<void* const*>(d_table);
   a.align = reinterpret_cast<const uint32_t*>(static_cast<char*>(d_table) +
@@ -354,6 +355,52 @@ int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate
   return hip_sqnorm(p, slot, dtype, sqnorm_dev, accumulate, stream);
 }
 
+int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream) {
+  GsRange range("gs_sqnorm_partial");
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  p->red_valid = true;
+  if (p->kind == GS_DEV_HOST) {
+    p->red_groups = 0;
+    return host_sqnorm(p, slot, dtype, &p->h_red, 0);
+  }
+  return hip_sqnorm_partial(p, slot, dtype, stream);
+}
+
+int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
+                     float coef_mul, float* out_dev) {
+  PLAN_OK(p);
+  if (!(max_norm > 0.f)) {
+    p->clip_on = false;
+    return GS_OK;
+  }
+  GS_CHECK_ARG(eps >= 0.f, "gs_plan_set_clip: eps < 0");
+  p->clip_on = true;
+  p->clip_own = sqnorm_dev == nullptr;
+  p->clip = ClipArgs{sqnorm_dev, 0, max_norm, eps, sq_mul, coef_mul, out_dev};
+  return GS_OK;
+}
+
+// the clip of the next update on plan p (nullptr: none)
+static int plan_clip(gs_plan* p, ClipArgs* c, const ClipArgs** out) {
+  *out = nullptr;
+  if (!p->clip_on) return GS_OK;
+  *c = p->clip;
+  if (p->clip_own) {
+    if (!p->red_valid)
+      return fail(GS_ESTATE, "clipped update from the plan's own Σg²: call gs_sqnorm_partial first");
+    if (p->kind == GS_DEV_HOST) {
+      c->sq = &p->h_red;
+      c->groups = 0;
+    } else {
+      c->groups = p->red_groups;
+      c->sq = p->red_groups > 0 ? hip_plan_red_groups(p) : hip_plan_red_scalar(p);
+    }
+  }
+  *out = c;
+  return GS_OK;
+}
+
 int gs_sum(gs_plan* p, int slot, int dtype, float* sum_dev, int accumulate, void* stream) {
   PLAN_OK(p);
   SLOT_OK(slot);
@@ -405,8 +452,11 @@ int gs_sgd_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double mo
     h.lr = p->hyper[0];
     if (h.first < 0) h.first = p->hyper[1] != 0.f;
   }
-  if (p->kind == GS_DEV_HOST) return host_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
-  return hip_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
+  ClipArgs cs;
+  const ClipArgs* clip;
+  GS_TRY_RET(plan_clip(p, &cs, &clip));
+  if (p->kind == GS_DEV_HOST) return host_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, clip);
+  return hip_sgd(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, clip, stream);
 }
 
 int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double beta1,
@@ -423,8 +473,11 @@ int gs_adam_step(gs_plan* p, int grad_dtype, int lowp_dtype, double lr, double b
     h.bc2s = p->hyper[1];
     h.decay = p->hyper[2];
   }
-  if (p->kind == GS_DEV_HOST) return host_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev);
-  return hip_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, stream);
+  ClipArgs cs;
+  const ClipArgs* clip;
+  GS_TRY_RET(plan_clip(p, &cs, &clip));
+  if (p->kind == GS_DEV_HOST) return host_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, clip);
+  return hip_adam(p, grad_dtype, lowp_dtype, h, grad_scale_dev, found_inf_dev, clip, stream);
 }
 
 int gs_plan_set_hyper_source(gs_plan* p, const float* hyper) {

@@ -375,6 +375,7 @@ class DistributedDataParallel(nn.Module):
         self._used_local = [0] * len(self._params) if find_unused_parameters else None
         self._ready_now: list = []
         self._overlap: dict | None = None  # _register_fused_optim state
+        self._param_index = {id(p): i for i, p in enumerate(self._params)}
         self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                               for i, p in enumerate(self._params)]
 
@@ -420,7 +421,7 @@ class DistributedDataParallel(nn.Module):
         for it in range(iters + 1):
             if on_dev:
                 torch.cuda.synchronize(self.device)
-            dist.barrier(group=self.process_group)
+            self._ctl_barrier()
             t0 = time.perf_counter()
             if self._comm is not None:
                 self._comm.all_reduce(buf, stream=L.stream_ptr(self.device))
@@ -432,21 +433,49 @@ class DistributedDataParallel(nn.Module):
             if it:
                 ts.append(time.perf_counter() - t0)
         ts.sort()
-        t = torch.tensor([ts[len(ts) // 2]], dtype=torch.float64,
-                         device=self.device if self._backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
-        return float(t.item())
+        return float(self._ctl_all_reduce(torch.tensor([ts[len(ts) // 2]], dtype=torch.float64), "max").item())
+
+    # ---- control-plane collectives (shape check, layout broadcast, checksums,
+    # calibration): on the libgsync communicator when there is one, so a rank
+    # runs ONE RCCL communicator — torch's ProcessGroupNCCL then issues nothing
+    # between wrap and training (T:nn/parallel/distributed.py:860-870 uses the
+    # process group for the same checks); the process group otherwise (gloo).
+    _CTL_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+    def _ctl_device(self):
+        return self.device if (self._comm is not None or self._backend == "nccl") else torch.device("cpu")
+
+    def _ctl_all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        t = t.to(self._ctl_device())
+        if self._comm is not None:
+            self._comm.all_reduce(t, op=op, stream=L.stream_ptr(self.device))
+        else:
+            dist.all_reduce(t, op=self._CTL_OPS[op], group=self.process_group)
+        return t
+
+    def _ctl_broadcast(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.to(self._ctl_device())
+        if self._comm is not None:
+            self._comm.broadcast(t, root=0, stream=L.stream_ptr(self.device))
+        else:
+            dist.broadcast(t, src=dist.get_global_rank(self.process_group, 0)
+                           if self.process_group is not dist.group.WORLD else 0, group=self.process_group)
+        return t
+
+    def _ctl_barrier(self):
+        if self._comm is not None:
+            self._ctl_all_reduce(torch.zeros(1, dtype=torch.int32))
+            torch.cuda.synchronize(self.device)
+        else:
+            dist.barrier(group=self.process_group)
 
     def _verify_param_shape_across_processes(self):
         if self.world_size == 1:
             return
-        dev = self.device if self._backend == "nccl" else torch.device("cpu")
         meta = torch.tensor([len(self._params), sum(p.numel() for p in self._params),
-                             hash(tuple(tuple(p.shape) for p in self._params)) % (2**61)],
-                            dtype=torch.int64, device=dev)
-        lo, hi = meta.clone(), meta.clone()
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.process_group)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.process_group)
+                             hash(tuple(tuple(p.shape) for p in self._params)) % (2**61)], dtype=torch.int64)
+        lo = self._ctl_all_reduce(meta.clone(), "min")
+        hi = self._ctl_all_reduce(meta.clone(), "max")
         if not torch.equal(lo, hi):
             raise RuntimeError("DDP expects same model across all ranks, but the parameter shapes differ "
                                f"(rank {self.rank}: {meta.tolist()})")
@@ -661,6 +690,15 @@ class DistributedDataParallel(nn.Module):
             elif self._comm is not None:
                 self._comm.all_reduce(buf, stream=L.stream_ptr(self.device))
                 self._pending[bi] = ("done", None)
+            elif buf.is_cuda and self._backend == "gloo":
+                # gloo over device buckets (ranks sharing a GPU: the rehearsal path).  Not
+                # gloo's own CUDA path: its async all-reduce of a device tensor issued from
+                # the autograd thread deadlocks at 4 ranks on one GPU in the second
+                # iteration (reproduced without libgsync: scripts/gloo_cuda_repro.py
+                # MODE=hook) — stage through host memory here instead
+                host = buf.to("cpu")  # waits for this bucket's pack on the producer stream
+                self._pending[bi] = ("host", (host, dist.all_reduce(host, group=self.process_group,
+                                                                    async_op=True)))
             else:
                 self._pending[bi] = ("work", dist.all_reduce(buf, group=self.process_group, async_op=True))
 
@@ -696,6 +734,10 @@ class DistributedDataParallel(nn.Module):
             kind, obj = self._pending[bi]
             if kind == "work":
                 obj.wait()
+            elif kind == "host":
+                host, work = obj
+                work.wait()
+                b.buffers[bi].copy_(host)
             elif kind == "fut":
                 res = obj.wait()
                 if isinstance(res, (list, tuple)):
@@ -738,20 +780,43 @@ class DistributedDataParallel(nn.Module):
         ``global_unused`` from the all-reduced local-used map; globally unused
         parameters keep their grad untouched).  One MAX all-reduce of the used
         map per iteration and a host read of it — torch's Reducer does the same."""
-        used = torch.tensor(self._used_local, dtype=torch.int32)
-        if self._comm is not None:
-            used = used.to(self.device)
-            self._comm.all_reduce(used, op="max", stream=L.stream_ptr(self.device))
-        else:
-            if self._backend == "nccl":
-                used = used.to(self.device)
-            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=self.process_group)
-        glob = used.tolist()
+        glob = self._ctl_all_reduce(torch.tensor(self._used_local, dtype=torch.int32), "max").tolist()
         b = self._bucketer
+        made = []
         for i, p in enumerate(self._params):
             if glob[i] and not self._used_local[i]:
                 view = b.bucket_view(i)
-                p.grad = view if self.gradient_as_bucket_view else view.clone(memory_format=torch.preserve_format)
+                if view.dtype != p.dtype:  # bf16/fp16 buckets: the grad keeps the parameter's dtype
+                    p.grad = view.to(p.dtype, memory_format=torch.preserve_format)
+                elif self.gradient_as_bucket_view:
+                    p.grad = view
+                else:
+                    p.grad = view.clone(memory_format=torch.preserve_format)
+                made.append(p.grad)
+        if made:
+            self._check_extra_grads(made)
+
+    def _check_extra_grads(self, grads):
+        """The fused checks of the bucket unpack (AMP non-finite flag, Σg²)
+        over grads created outside it — those of parameters unused on this rank
+        (their slots are not unpacked): every rank's flag then covers the same
+        averaged grads, so every rank takes the same skip decision."""
+        if self._found_inf_target is None and self._sqnorm_target is None:
+            return
+        by_dtype: dict = {}
+        for g in grads:
+            by_dtype.setdefault(g.dtype, []).append(g)
+        cache = self.__dict__.setdefault("_extra_plans", {})
+        for dt, gs in by_dtype.items():
+            key = (dt,) + tuple(g.numel() for g in gs)
+            plan = cache.get(key)
+            if plan is None:
+                plan = cache[key] = TensorListPlan([g.numel() for g in gs], self.device)
+            plan.set_ptrs(0, gs)
+            if self._found_inf_target is not None:
+                plan.unscale_check(0, dt, None, self._found_inf_target)
+            if self._sqnorm_target is not None:
+                plan.sqnorm(0, dt, self._sqnorm_target, accumulate=True)
 
     def _maybe_rebuild_buckets(self):
         if self._has_rebuilt_buckets or not (self.static_graph or not self.find_unused_parameters):
@@ -776,14 +841,10 @@ class DistributedDataParallel(nn.Module):
         """Broadcast rank 0's rebuilt layout (Reducer::sync_bucket_indices)."""
         if self.world_size == 1:
             return buckets
-        dev = self.device if self._backend == "nccl" else torch.device("cpu")
         n = len(self._params)
         flat = [len(buckets)] + [len(b) for b in buckets] + [i for b in buckets for i in b]
         flat += [0] * (2 * n + 1 - len(flat))
-        t = torch.tensor(flat, dtype=torch.int64, device=dev)
-        src = dist.get_global_rank(self.process_group, 0) if self.process_group is not dist.group.WORLD else 0
-        dist.broadcast(t, src=src, group=self.process_group)
-        v = t.tolist()
+        v = self._ctl_broadcast(torch.tensor(flat, dtype=torch.int64)).tolist()
         nb = v[0]
         counts = v[1:1 + nb]
         out, pos = [], 1 + nb
@@ -819,9 +880,29 @@ class DistributedDataParallel(nn.Module):
                 if st is None:
                     st = ov["streams"][ptr.value] = torch.cuda.ExternalStream(ptr.value, device=self.device)
                 with torch.cuda.stream(st):
-                    bo.step()
+                    self._step_bucket(bi, bo)
             else:
-                bo.step()
+                self._step_bucket(bi, bo)
+
+    def _step_bucket(self, bi, bo):
+        """One overlapped update of bucket bi.  As torch's _hook_then_optimizer
+        (T:distributed/algorithms/ddp_comm_hooks/optimizer_overlap_hooks.py), every
+        bucket parameter steps with its bucket gradient — a parameter unused on
+        this rank (find_unused_parameters / static_graph: no grad yet) with the
+        averaged one from the bucket view (zeros when unused everywhere), so weight
+        decay and momentum apply on every rank alike.  Runs on the bucket's stream,
+        behind its chain; the temporary grads are dropped after the launch
+        (_grads_of_locally_unused creates the kept ones at finalize)."""
+        tmp = []
+        for p in bo.param_groups[0]["params"]:
+            if p.grad is None:
+                i = self._param_index[id(p)]
+                view = self._bucketer.bucket_view(i)
+                p.grad = view if view.dtype == p.dtype else view.to(p.dtype, memory_format=torch.preserve_format)
+                tmp.append(p)
+        bo.step()
+        for p in tmp:
+            p.grad = None
 
     # ------------------------------------------------------------------ API
     def _register_fused_optim(self, optim: type, *args, optim_params=None, **kwargs):
@@ -940,13 +1021,11 @@ class DistributedDataParallel(nn.Module):
         Raises RuntimeError naming the first bad bucket; returns per bucket
         (Σ_r pre, post, tolerance)."""
         sums = self._debug_sums.view(-1, 3).double()
-        dev = self.device if self._backend == "nccl" else torch.device("cpu")
-        pre, post, sq = sums[:, 0].to(dev), sums[:, 1].to(dev), sums[:, 2].to(dev)
-        tot, sqt, lo, hi = pre.clone(), sq.clone(), post.clone(), post.clone()
-        dist.all_reduce(tot, group=self.process_group)
-        dist.all_reduce(sqt, group=self.process_group)
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.process_group)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.process_group)
+        pre, post, sq = sums[:, 0].contiguous(), sums[:, 1].contiguous(), sums[:, 2].contiguous()
+        tot = self._ctl_all_reduce(pre.clone(), "sum")
+        sqt = self._ctl_all_reduce(sq.clone(), "sum")
+        lo = self._ctl_all_reduce(post.clone(), "min")
+        hi = self._ctl_all_reduce(post.clone(), "max")
         out = []
         for bi, buf in enumerate(self._bucketer.buffers):
             tol = rtol * (buf.numel() * float(sqt[bi])) ** 0.5 + 1e-30
@@ -1011,6 +1090,24 @@ class DistributedDataParallel(nn.Module):
 
     def bucket_indices(self):
         return [list(b) for b in self._bucketer.buckets]
+
+    def close(self):
+        """Detach from the module: remove the gradient hooks and free the
+        buckets (the module can then be wrapped again, e.g. with another
+        bucket policy).  Not collective."""
+        for h in getattr(self, "_hook_handles", []):
+            try:
+                h.remove()
+            except Exception:  # pragma: no cover
+                pass
+        self._hook_handles = []
+        b = getattr(self, "_bucketer", None)
+        if b is not None:
+            if self.gradient_as_bucket_view:
+                for p in self._params:  # grads must not alias the buckets about to be freed
+                    if p.grad is not None:
+                        p.grad = p.grad.clone()
+            b.close()
 
     def __del__(self):
         for h in getattr(self, "_hook_handles", []):

@@ -153,6 +153,29 @@ class TensorListPlan:
             "gs_sqnorm",
         )
 
+    def sqnorm_partial(self, slot, dtype, stream=None):
+        """Σ x² of the slot left inside the plan (gs_sqnorm_partial): no combine
+        launch; the next clipped sgd()/adam() on this plan folds it."""
+        L.check(L.lib().gs_sqnorm_partial(self.handle, slot, L.gs_dtype(dtype), self._stream(stream)),
+                "gs_sqnorm_partial")
+
+    def set_clip(self, max_norm: float | None, eps: float = 1e-6, sqnorm: torch.Tensor | None = None,
+                 sq_mul: float = 1.0, coef_mul: float = 1.0, out: torch.Tensor | None = None):
+        """Fold the clip coefficient min(1, max_norm/(‖g‖+eps)) into the later
+        sgd()/adam() launches of this plan (gs_plan_set_clip): ‖g‖² from
+        ``sqnorm`` (a 1-element fp32 tensor) or, when None, from this plan's last
+        :meth:`sqnorm_partial`; ``out`` (fp32[3], optional) receives
+        [‖g‖², coef, ‖g‖].  ``max_norm`` None/0 turns it off."""
+        for t in (sqnorm, out):
+            if t is not None and (t.dtype != torch.float32 or (t.device.type == "cuda") != (self.kind == L.GS_DEV_HIP)):
+                raise ValueError("clip tensors: fp32, where the plan runs")
+        if out is not None and out.numel() < 3:
+            raise ValueError("clip out: 3 elements")
+        L.check(L.lib().gs_plan_set_clip(self.handle, None if sqnorm is None else sqnorm.data_ptr(),
+                                         float(max_norm or 0.0), float(eps), float(sq_mul), float(coef_mul),
+                                         None if out is None else out.data_ptr()), "gs_plan_set_clip")
+        self._clip_refs = (sqnorm, out)
+
     def sum(self, slot, dtype, out: torch.Tensor, accumulate=False, stream=None):
         """out[0] = Σ x over the slot's tensors (fp32, deterministic order)."""
         L.check(

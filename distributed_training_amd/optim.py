@@ -32,12 +32,18 @@ buffer outside the graph, so LR schedulers keep working across replays.
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterable
 
 import torch
 
 from . import _lib as L
 from .multi_tensor import TensorListPlan, clip_coef, is_dense, update_task_units
+
+
+# the gradient-norm clip folded into the update kernels (gs_plan_set_clip);
+# GSYNC_CLIP_FUSED=0 keeps the separate Σg² / coefficient launches (A/B runs)
+CLIP_FUSED = os.environ.get("GSYNC_CLIP_FUSED", "1") not in ("", "0")
 
 
 def _capturing() -> bool:
@@ -152,22 +158,51 @@ class _FusedBase(torch.optim.Optimizer):
 
     def _clip_scale(self, device, all_plans):
         """DeepSpeed-style gradient_clipping folded into the update: returns the
-        device coefficient min(1, max_norm/(‖g‖+1e-6)) (times grad_scale)."""
+        grad multiplier the update launches get.
+
+        Folded path (default): the coefficient min(1, max_norm/(‖g‖+1e-6))
+        (times grad_scale) is formed by the update kernel's own workgroups
+        (gs_plan_set_clip) — one plan: from the plan's Σg² partial sums
+        (gs_sqnorm_partial), so Σg² -> update is two launches with no combine
+        and no coefficient launch between them; several plans (grad dtypes):
+        Σg² accumulated into one scalar first.  Bit-identical to the separate
+        path (GSYNC_CLIP_FUSED=0: Σg² + combine, gs_clip_coef, mul_ launches)."""
         max_norm = self.defaults.get("max_grad_norm")
         if not max_norm:
+            for plan, _ in all_plans:
+                if getattr(plan, "_clip_on", False):
+                    plan.set_clip(None)
+                    plan._clip_on = False
             return self.grad_scale
         buf = self._clip_buf.get(device)
         if buf is None:
             buf = torch.zeros(3, dtype=torch.float32, device=device)
             self._clip_buf[device] = buf
         sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
+        self.last_grad_norm = norm
+        if CLIP_FUSED:
+            if len(all_plans) == 1:
+                plan, gdt = all_plans[0]
+                plan.sqnorm_partial(1, gdt)
+                plan.set_clip(float(max_norm), 1e-6, None, out=buf)
+                plan._clip_on = True
+            else:
+                for i, (plan, gdt) in enumerate(all_plans):
+                    plan.sqnorm(1, gdt, sq, accumulate=i > 0)
+                for plan, _ in all_plans:
+                    plan.set_clip(float(max_norm), 1e-6, sq, out=buf)
+                    plan._clip_on = True
+            return self.grad_scale  # the kernels fold it into the coefficient
+        for plan, _ in all_plans:
+            if getattr(plan, "_clip_on", False):
+                plan.set_clip(None)
+                plan._clip_on = False
         for i, (plan, gdt) in enumerate(all_plans):
             plan.sqnorm(1, gdt, sq, accumulate=i > 0)
         if self.grad_scale is not None:
             # norm of the unscaled grads: ‖g·s‖² = s²‖g‖²
             sq.mul_(self.grad_scale * self.grad_scale)
         clip_coef(sq, float(max_norm), 1e-6, coef, norm)
-        self.last_grad_norm = norm
         if self.grad_scale is not None:
             coef.mul_(self.grad_scale)
         return coef
@@ -288,18 +323,76 @@ class FusedAdam(_FusedBase):
                         fused=fused, decoupled_weight_decay=adamw, max_grad_norm=max_grad_norm)
         super().__init__(params, defaults)
 
+    # ---- device step counters (capturable / AMP): one fp64 counter per cohort of
+    # parameters that have advanced together so far.  torch keeps one step per
+    # parameter (T:optim/adam.py: state_steps[i] += 1 only for params with a
+    # grad); a cohort shares one counter while all its members get grads, and is
+    # split (its counter cloned on the device, no host read) the first step some
+    # members have none — so every parameter's bias correction is its own.
+    def _adopt_cohorts(self, h, group):
+        """Give every stateful parameter of `group` without a device counter one:
+        parameters whose (host) step values are equal share a new cohort."""
+        cohorts = h.setdefault("cohorts", {})
+        by_value: dict = {}
+        for p in group["params"]:
+            st = self.state.get(p)
+            if not st or "exp_avg" not in st:
+                continue
+            t = st.get("step")
+            if t is not None and id(t) in cohorts:
+                continue
+            if _capturing():
+                raise RuntimeError("FusedAdam: state must exist before capture (take an eager step first)")
+            v = 0.0 if t is None else float(t)
+            c = by_value.get(v)
+            if c is None:
+                c = by_value[v] = {"step": torch.full((1,), v, dtype=torch.float64, device=p.device),
+                                   "hyper": torch.zeros(3, dtype=torch.float32, device=p.device),
+                                   "members": set()}
+                cohorts[id(c["step"])] = c
+            c["members"].add(id(p))
+            st["step"] = c["step"]
+
+    def _split_cohort(self, h, c, ps):
+        """Members `ps` (with grads) leave cohort `c` (some of whose members have
+        none this step) for a new one starting at the same count."""
+        if _capturing():
+            raise RuntimeError("FusedAdam: the set of parameters with grads changed inside a capture")
+        n = {"step": c["step"].clone(), "hyper": torch.zeros_like(c["hyper"]), "members": {id(p) for p in ps}}
+        c["members"] -= n["members"]
+        h["cohorts"][id(n["step"])] = n
+        for p in ps:
+            self.state[p]["step"] = n["step"]
+        return n
+
+    def state_dict(self):
+        """torch's layout: one ``step`` tensor per parameter (fp32; on the CPU,
+        or on the device when capturable, as torch's Adam keeps it) — device
+        counters shared by a cohort are read out here (host read, checkpoint time)."""
+        sd = super().state_dict()
+        vals: dict = {}
+        for k, st in list(sd["state"].items()):
+            t = st.get("step")
+            if torch.is_tensor(t) and t.dtype == torch.float64:
+                v = vals.get(id(t))
+                if v is None:
+                    v = vals[id(t)] = float(t.item())
+                dev = t.device if self.capturable else torch.device("cpu")
+                sd["state"][k] = dict(st, step=torch.tensor(v, dtype=torch.float32, device=dev))
+        return sd
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        cap = self._device_state()  # device step counter: capturable or AMP (no host read of found_inf)
+        cap = self._device_state()  # device step counters: capturable or AMP (no host read of found_inf)
         work = []
         for gi, group in enumerate(self.param_groups):
             buckets = {}
+            by_cohort: dict = {}
             h = None
-            start = len(work)
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -309,13 +402,6 @@ class FusedAdam(_FusedBase):
                 if p.dtype != torch.float32:
                     raise RuntimeError("FusedAdam expects fp32 parameters (keep a fp32 master copy)")
                 st = self.state[p]
-                if cap:
-                    if h is None:
-                        h = self._group_hyper(gi, group, p.device)
-                    if "step" not in h:  # one device counter per group, from the (loaded) state
-                        s0 = next((float(self.state[q]["step"]) for q in group["params"]
-                                   if "step" in self.state[q]), 0.0)
-                        h["step"] = torch.full((1,), s0, dtype=torch.float64, device=p.device)
                 if len(st) == 0 or "exp_avg" not in st:
                     if _capturing():
                         raise RuntimeError("FusedAdam: state must exist before capture (take an eager step first)")
@@ -323,27 +409,44 @@ class FusedAdam(_FusedBase):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 if cap:
-                    st["step"] = h["step"]  # shared device counter, advanced by gs_adam_hyper
-                    key = (p.grad.dtype, None)
+                    if h is None:
+                        h = self._group_hyper(gi, group, p.device)
+                    if id(st["step"]) not in h.get("cohorts", {}):
+                        self._adopt_cohorts(h, group)
+                    by_cohort.setdefault(id(st["step"]), []).append(p)
                 else:
                     st["step"] += 1
-                    key = (p.grad.dtype, float(st["step"].item()))
-                lists = buckets.setdefault(key, ([], [], [], []))
-                lists[0].append(p)
-                lists[1].append(p.grad)
-                lists[2].append(st["exp_avg"])
-                lists[3].append(st["exp_avg_sq"])
+                    lists = buckets.setdefault((p.grad.dtype, float(st["step"].item())), ([], [], [], []))
+                    lists[0].append(p)
+                    lists[1].append(p.grad)
+                    lists[2].append(st["exp_avg"])
+                    lists[3].append(st["exp_avg_sq"])
+            for cid, ps in by_cohort.items():
+                c = h["cohorts"][cid]
+                if len(ps) < len(c["members"]):
+                    c = self._split_cohort(h, c, ps)
+                work.append((group, None, gi, (h, c)))  # advance the cohort's counter, form its hyper source
+                for p in ps:
+                    st = self.state[p]
+                    lists = buckets.setdefault((p.grad.dtype, id(c["step"])), ([], [], [], []))
+                    lists[0].append(p)
+                    lists[1].append(p.grad)
+                    lists[2].append(st["exp_avg"])
+                    lists[3].append(st["exp_avg_sq"])
+            cohort_hyper = {id(c["step"]): c["hyper"] for c in h["cohorts"].values()} if h is not None else {}
             for (gdt, step), (ps, gs, ms, vs) in buckets.items():
                 plan = self._plans.get(ps)
                 plan.set_ptrs(0, ps)
                 plan.set_ptrs(1, gs)
                 plan.set_ptrs(2, ms)
                 plan.set_ptrs(3, vs)
-                if cap and getattr(plan, "_hyper", None) is not h["hyper"]:
-                    plan.set_hyper_source(h["hyper"])
-                work.append((group, plan, gdt, step))
-            if cap and h is not None:  # before the group's update launches
-                work.insert(start, (group, None, gi, h))
+                if cap:
+                    hyper = cohort_hyper[step]
+                    if getattr(plan, "_hyper", None) is not hyper:
+                        plan.set_hyper_source(hyper)
+                    work.append((group, plan, gdt, None))
+                else:
+                    work.append((group, plan, gdt, step))
         if not work:
             return loss
         if cap:
@@ -354,13 +457,13 @@ class FusedAdam(_FusedBase):
         scale = self._clip_scale(plans[0][0].device, plans)
         for group, plan, gdt, step in work:
             beta1, beta2 = group["betas"]
-            if plan is None:  # capturable: advance the group's device step, form its hyper source
-                h = step
+            if plan is None:  # device counters: advance the cohort's step, form its hyper source
+                h, c = step
                 L.check(L.lib().gs_adam_hyper(
-                    L.GS_DEV_HIP if h["step"].is_cuda else L.GS_DEV_HOST, h["step"].data_ptr(), h["lr"].data_ptr(),
+                    L.GS_DEV_HIP if c["step"].is_cuda else L.GS_DEV_HOST, c["step"].data_ptr(), h["lr"].data_ptr(),
                     float(beta1), float(beta2), float(group["weight_decay"]),
-                    None if self.found_inf is None else self.found_inf.data_ptr(), h["hyper"].data_ptr(),
-                    L.stream_ptr(h["step"].device) if h["step"].is_cuda else None), "gs_adam_hyper")
+                    None if self.found_inf is None else self.found_inf.data_ptr(), c["hyper"].data_ptr(),
+                    L.stream_ptr(c["step"].device) if c["step"].is_cuda else None), "gs_adam_hyper")
                 continue
             if step is None:  # the kernel reads step_size / bc2 / decay from the hyper source
                 plan.adam(gdt, group["lr"], beta1, beta2, group["eps"], group["weight_decay"],

@@ -37,6 +37,7 @@ from . import _lib as L
 from .comm import get_communicator
 from .ddp import BUCKET_ALIGN_ELEMS, compute_bucket_assignment_by_size
 from .multi_tensor import TensorListPlan, clip_coef, dense_like_param, update_task_units
+from . import optim as _optim
 
 
 class DynamicLossScaler:
@@ -130,7 +131,8 @@ class ZeroDataParallel:
         self._in_backward = False
         self._queued = False
         self._pending = {}
-        self._scratch = torch.zeros(4, dtype=torch.float32, device=self.device)
+        # [found_inf, Σg² (all-reduced), 1/scale, -, clip out: Σg²·s², coefficient, ‖g‖]
+        self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
 
     # ------------------------------------------------------------------ setup
@@ -253,8 +255,14 @@ class ZeroDataParallel:
                                                    ctypes.byref(self._n_ready)), "gs_bucketer_mark_ready")
             for k in range(self._n_ready.value):
                 b = self._ready[k]
-                if self._comm is None:
-                    self._pending[b] = dist.all_reduce(self.grad_bufs[b], group=self.pg, async_op=True)
+                if self._comm is None and self.grad_bufs[b].is_cuda:
+                    # device buckets over gloo (the rehearsal path): staged through host
+                    # memory, as DDP does (gloo's async CUDA path deadlocks from the
+                    # autograd thread at 4 ranks on one GPU)
+                    host = self.grad_bufs[b].to("cpu")
+                    self._pending[b] = (host, dist.all_reduce(host, group=self.pg, async_op=True))
+                elif self._comm is None:
+                    self._pending[b] = (None, dist.all_reduce(self.grad_bufs[b], group=self.pg, async_op=True))
                 for held in self._held.pop(b, []):
                     if self._comm is not None:
                         # the pack on the comm stream is enqueued: the allocator may
@@ -265,7 +273,10 @@ class ZeroDataParallel:
 
     def _finalize(self):
         for b in sorted(self._pending):
-            self._pending[b].wait()
+            host, work = self._pending[b]
+            work.wait()
+            if host is not None:
+                self.grad_bufs[b].copy_(host)
         self._pending = {}
         L.check(L.lib().gs_bucketer_finalize(self.handle, self._stream), "gs_bucketer_finalize")
         self._in_backward = False
@@ -289,14 +300,28 @@ class ZeroDataParallel:
             found_inf.zero_()
             self.plan.unscale_check(1, self.dtype, None, found_inf)
             self._allreduce_scalar(found_inf, "max")
-        if self.clip > 0:
+        if self.clip > 0 and _optim.CLIP_FUSED:
+            # DeepSpeed gradient_clipping (R:resnet/deepspeed/deepspeed_train.py:195) folded
+            # into the update: its workgroups form min(1, c/(‖g‖+1e-6))·(1/scale) themselves
+            # (gs_plan_set_clip) — no coefficient launch; one rank: Σg² stays as the plan's
+            # partial sums (no combine launch either)
+            if self.world == 1:
+                self.plan.sqnorm_partial(1, self.dtype)
+                self.plan.set_clip(self.clip, 1e-6, None, inv_scale * inv_scale, inv_scale, out=s[4:7])
+            else:
+                sq = s[1:2]
+                self.plan.sqnorm(1, self.dtype, sq)
+                self._allreduce_scalar(sq, "sum")
+                self.plan.set_clip(self.clip, 1e-6, sq, inv_scale * inv_scale, inv_scale, out=s[4:7])
+        elif self.clip > 0:
+            self.plan.set_clip(None)
             sq = s[1:2]
             self.plan.sqnorm(1, self.dtype, sq)
             self._allreduce_scalar(sq, "sum")
             if inv_scale != 1.0:
                 sq.mul_(inv_scale * inv_scale)
-            clip_coef(sq, self.clip, 1e-6, s[2:3], s[3:4])
-            grad_scale = s[2:3]
+            clip_coef(sq, self.clip, 1e-6, s[5:6], s[6:7])
+            grad_scale = s[5:6]
             if inv_scale != 1.0:
                 grad_scale.mul_(inv_scale)
         elif inv_scale != 1.0:
@@ -331,7 +356,8 @@ class ZeroDataParallel:
             p.grad = None
 
     def grad_norm(self):
-        return self._scratch[3:4]
+        """‖g‖ of the unscaled averaged grads at the last clipped step (device tensor)."""
+        return self._scratch[6:7]
 
     def state_dict(self):
         """This rank's optimizer shard (fp32 master + states): DeepSpeed's

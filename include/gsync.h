@@ -203,6 +203,27 @@ int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate
 /* Σ x over every tensor of a slot (fp32 accumulation, deterministic order):
  * the bucket checksum of the GSYNC_DEBUG mode (gs_bucketer_set_debug) */
 int gs_sum(gs_plan* p, int slot, int dtype, float* sum_dev, int accumulate, void* stream);
+/* Σ x² of one slot left inside the plan as partial sums (no combine launch,
+ * nothing written to caller memory), for the next clipped gs_sgd_step /
+ * gs_adam_step on the same plan and stream (gs_plan_set_clip with
+ * sqnorm_dev = NULL): the update's workgroups fold the partials themselves.
+ * replaces: T:nn/utils/clip_grad.py:96-109 (_foreach_norm + the norm of norms)
+ *           when the norm only feeds the clip */
+int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream);
+/* Gradient-norm clip folded into every later gs_sgd_step / gs_adam_step on
+ * this plan (max_norm <= 0 turns it off).  The update forms, in every workgroup,
+ *   sq   = sqnorm_dev[0]   (sqnorm_dev = NULL: the plan's gs_sqnorm_partial sums)
+ *   sq  *= grad_scale² (if grad_scale_dev) * sq_mul;  norm = sqrt(sq)
+ *   coef = min(1, max_norm/(norm + eps)) * grad_scale * coef_mul
+ * and multiplies the grads by coef — the arithmetic of gs_clip_coef plus the
+ * caller's scale multiplies, bit for bit, without the coefficient launch.
+ * out_dev (nullable, fp32[3]) receives [sq, coef, norm] (written even when
+ * found_inf skips the step).  sq_mul / coef_mul: host-side loss-scale factors
+ * (ZeRO: (1/scale)², 1/scale), 1 = none.
+ * replaces: T:nn/utils/clip_grad.py:165-174 (clip_coef, clamp, _foreach_mul_)
+ *           DeepSpeed gradient_clipping (R:resnet/deepspeed/deepspeed_train.py:195) */
+int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
+                     float coef_mul, float* out_dev);
 /* coef_dev[0] = min(1, max_norm / (sqrt(sqnorm_dev[0]) + eps)); norm_dev (nullable) = sqrt
  * replaces: T:nn/utils/clip_grad.py:165-174 clip_coef / clamp */
 int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,

@@ -11,6 +11,8 @@ Tolerances: SGD rtol 1e-6 / atol 1e-7 (fp32, fma placement may differ from
 ATen's in the last bit); Adam atol lr*1e-3 (its sign can flip
 where |g| ~ eps).
 """
+import copy
+
 import pytest
 import torch
 import torch.nn as nn
@@ -25,7 +27,7 @@ def _micro():
     return ResNet(BasicBlock, [1, 1, 1, 1], num_classes=10, width=8)
 
 
-def _run(dev, kind, poison_at, iters=5):
+def _run(dev, kind, poison_at, iters=5, drop=None):
     torch.manual_seed(0)
     m1, m2 = _micro().to(dev), _micro().to(dev)
     m2.load_state_dict(m1.state_dict())
@@ -50,6 +52,9 @@ def _run(dev, kind, poison_at, iters=5):
             next(m1.parameters()).grad.view(-1)[3] = float("inf")
         for p1, p2 in zip(m1.parameters(), m2.parameters()):
             p2.grad = p1.grad.detach().clone()
+        for k in (drop or {}).get(it, ()):  # a parameter without a grad this step
+            list(m1.parameters())[k].grad = None
+            list(m2.parameters())[k].grad = None
         s1.step(o1)
         s1.update()
         s2.step(o2)
@@ -67,6 +72,60 @@ def _run(dev, kind, poison_at, iters=5):
             torch.testing.assert_close(st1["momentum_buffer"], st2["momentum_buffer"], rtol=1e-6, atol=1e-7)
         else:
             assert float(st1["step"]) == float(st2["step"])
+    if kind == "adam":
+        # state_dict: one fp32 step tensor per parameter, as torch's (no shared device counter)
+        sd1, sd2 = o1.state_dict(), o2.state_dict()
+        steps = [st["step"] for st in sd1["state"].values()]
+        assert len({id(t) for t in steps}) == len(steps)
+        for k in sd2["state"]:
+            t1, t2 = sd1["state"][k]["step"], sd2["state"][k]["step"]
+            assert t1.dtype == torch.float32 and t1.device.type == "cpu" and float(t1) == float(t2)
+
+
+# parameters that get no grad on some steps keep their own
+# Adam step count (torch advances state["step"] per parameter, only with a grad)
+DROPS = {1: (0, 5), 2: (5,), 3: (1,)}
+
+
+@pytest.mark.parametrize("poison_at", [(), (2,)])
+def test_scaler_cpu_intermittent_grads(poison_at):
+    _run(torch.device("cpu"), "adam", poison_at, iters=6, drop=DROPS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("poison_at", [(), (2,)])
+def test_scaler_gpu_intermittent_grads(cuda_device, poison_at):
+    _run(cuda_device, "adam", poison_at, iters=6, drop=DROPS)
+
+
+def test_adam_device_counters_from_loaded_state():
+    """A torch Adam state_dict whose parameters are at different steps, loaded
+    into FusedAdam on the AMP (device-counter) path: each parameter continues
+    from its own step, bit-for-bit with torch.optim.Adam continuing the same."""
+    torch.manual_seed(0)
+    ps_t = [torch.nn.Parameter(torch.randn(n)) for n in (10, 33, 7)]
+    ps_f = [torch.nn.Parameter(p.detach().clone()) for p in ps_t]
+    ot = torch.optim.Adam(ps_t, lr=1e-2)
+    g = torch.Generator().manual_seed(1)
+    for it in range(4):  # param 1 skips two steps: steps 4 / 2 / 4
+        for k, p in enumerate(ps_t):
+            p.grad = None if (k == 1 and it in (1, 2)) else torch.randn(p.shape, generator=g)
+        ot.step()
+    of = FusedAdam(ps_f, lr=1e-2)
+    of.load_state_dict(copy.deepcopy(ot.state_dict()))  # torch's state_dict shares its step tensors
+    of.found_inf = torch.zeros(1)  # the AMP path: device counters
+    for p, q in zip(ps_f, ps_t):
+        p.data.copy_(q.data)
+    for it in range(3):
+        for p, q in zip(ps_t, ps_f):
+            p.grad = torch.randn(p.shape, generator=g)
+            q.grad = p.grad.clone()
+        ot.step()
+        of.step()
+        for k, (p, q) in enumerate(zip(ps_t, ps_f)):
+            torch.testing.assert_close(q, p, rtol=0, atol=1e-2 * 1e-3, msg=lambda m: f"it {it} param {k}: {m}")
+    sd = of.state_dict()
+    assert [float(sd["state"][k]["step"]) for k in range(3)] == [7.0, 5.0, 7.0]
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])

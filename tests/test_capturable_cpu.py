@@ -63,7 +63,8 @@ def test_adam_hyper_vs_oracle_formula():
     for k in range(1, 6):
         ps[0].grad = torch.ones(4)
         opt.step()
-        h = opt._dev_hyper[0]["hyper"]
+        (cohort,) = opt._dev_hyper[0]["cohorts"].values()  # one device step counter: every param has a grad
+        h = cohort["hyper"]
         bc1, bc2 = 1 - 0.8 ** k, 1 - 0.95 ** k
         exp = np.array([(3e-3 / bc1) * -1, bc2 ** 0.5, 1 - 3e-3 * 0.1], dtype=np.float32)
         assert np.array_equal(h.numpy(), exp)

@@ -1,0 +1,147 @@
+"""The gradient-norm clip folded into the update kernels (gs_plan_set_clip /
+gs_sqnorm_partial) against the separate path it replaces (Σg² + combine,
+gs_clip_coef, the mul_ launches; optim.CLIP_FUSED = False): bit-identical
+parameters, optimizer state and published norm, for SGD and Adam, with and
+without an AMP grad scale, a skipped (found_inf) step, and ZeRO's loss-scale
+multipliers.  Reference arithmetic: T:nn/utils/clip_grad.py:165-174 (coef),
+DeepSpeed gradient_clipping R:resnet/deepspeed/deepspeed_train.py:195.
+
+CPU tests run the host backend; the `gpu` ones the gfx950 kernels, where the
+folded coefficient comes from the Σg² kernel's 64 group sums."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+import distributed_training_amd as D
+from distributed_training_amd import optim as O
+
+SIZES = [1000, 64, 4099, 3, 70001, 17, 2 ** 16, 1]
+
+
+def _params(dev, seed=0, sizes=SIZES):
+    g = torch.Generator().manual_seed(seed)
+    ps = [torch.nn.Parameter(torch.randn(n, generator=g).to(dev)) for n in sizes]
+    for p in ps:
+        p.grad = (torch.randn(p.shape, generator=g) * 0.3).to(dev)
+    return ps
+
+
+def _run(dev, fused, opt_cls, kw, gscale=None, found_inf=None, steps=3):
+    old = O.CLIP_FUSED
+    O.CLIP_FUSED = fused
+    try:
+        ps = _params(dev)
+        opt = opt_cls(ps, max_grad_norm=1.0, **kw)
+        if gscale is not None:
+            opt.grad_scale = torch.tensor([gscale], device=dev)
+        if found_inf is not None:
+            opt.found_inf = torch.tensor([found_inf], device=dev)
+        norms = []
+        for s in range(steps):
+            for i, p in enumerate(ps):
+                p.grad.mul_(1.0 + 0.25 * s)  # a different norm every step
+            opt.step()
+            norms.append(opt.last_grad_norm.clone())
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        state = [(k, v.clone()) for p in ps for k, v in sorted(opt.state[p].items()) if torch.is_tensor(v)]
+        return [p.detach().clone() for p in ps], state, torch.cat(norms)
+    finally:
+        O.CLIP_FUSED = old
+
+
+def _assert_same(a, b):
+    pa, sa, na = a
+    pb, sb, nb = b
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    for (k1, x), (k2, y) in zip(sa, sb):
+        assert k1 == k2 and torch.equal(x.float().cpu(), y.float().cpu()), k1
+    assert torch.equal(na, nb)
+
+
+CASES = [
+    (D.FusedSGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+    (D.FusedAdam, dict(lr=1e-3)),
+    (D.FusedAdamW, dict(lr=1e-3, weight_decay=0.01)),
+]
+
+
+@pytest.mark.parametrize("opt_cls,kw", CASES)
+@pytest.mark.parametrize("gscale", [None, 0.125])
+def test_folded_clip_equals_separate_path_cpu(opt_cls, kw, gscale):
+    dev = torch.device("cpu")
+    _assert_same(_run(dev, True, opt_cls, kw, gscale), _run(dev, False, opt_cls, kw, gscale))
+
+
+def test_folded_clip_skipped_step_cpu():
+    dev = torch.device("cpu")
+    fused = _run(dev, True, D.FusedSGD, CASES[0][1], 0.5, found_inf=1.0)
+    sep = _run(dev, False, D.FusedSGD, CASES[0][1], 0.5, found_inf=1.0)
+    _assert_same(fused, sep)
+    assert torch.equal(fused[0][0], _params(dev)[0].detach())  # nothing moved
+
+
+def test_plan_clip_needs_partial_first():
+    plan = D.multi_tensor.TensorListPlan([8], torch.device("cpu"), task_units=0)
+    p, g, b = torch.zeros(8), torch.ones(8), torch.zeros(8)
+    plan.set_ptrs(0, [p])
+    plan.set_ptrs(1, [g])
+    plan.set_ptrs(2, [b])
+    plan.set_clip(1.0)
+    with pytest.raises(D._lib.GsyncError, match="gs_sqnorm_partial"):
+        plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    plan.sqnorm_partial(1, torch.float32)
+    out = torch.zeros(3)
+    plan.set_clip(1.0, out=out)
+    plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    # ‖g‖ = sqrt(8): coef = 1/(sqrt(8)+1e-6); p = -0.1 * coef
+    nrm = torch.tensor(8.0).sqrt()
+    coef = torch.clamp(1.0 / (nrm + 1e-6), max=1.0)
+    assert torch.equal(out, torch.stack([torch.tensor(8.0), coef, nrm]))
+    assert torch.equal(p, torch.full((8,), 1.0) * coef * -0.1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt_cls,kw", CASES)
+@pytest.mark.parametrize("gscale", [None, 0.125])
+def test_folded_clip_equals_separate_path_gpu(opt_cls, kw, gscale):
+    dev = torch.device("cuda", 0)
+    _assert_same(_run(dev, True, opt_cls, kw, gscale), _run(dev, False, opt_cls, kw, gscale))
+
+
+@pytest.mark.gpu
+def test_folded_clip_skipped_step_gpu():
+    dev = torch.device("cuda", 0)
+    _assert_same(_run(dev, True, D.FusedAdam, dict(lr=1e-3), 0.5, found_inf=1.0),
+                 _run(dev, False, D.FusedAdam, dict(lr=1e-3), 0.5, found_inf=1.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mixed", [False, True])
+def test_folded_clip_large_plan_gpu(mixed):
+    """ResNet-50-sized single plan (25.6 M elements: the Σg² kernel's full 64
+    groups), and with one bf16 grad (two plans: the accumulated-scalar form)."""
+    dev = torch.device("cuda", 0)
+    sizes = [2048 * 1000, 1000, 512 * 2048, 2048, 2048 * 512 * 9, 64 * 3 * 49, 7, 2048 * 4096]
+    res = []
+    try:
+        for fused in (True, False):
+            O.CLIP_FUSED = fused
+            g = torch.Generator(device=dev).manual_seed(3)
+            ps = [torch.nn.Parameter(torch.randn(n, device=dev, generator=g)) for n in sizes]
+            for p in ps:
+                p.grad = torch.randn(p.shape, device=dev, generator=g) * 0.01
+            if mixed:
+                ps[1].grad = ps[1].grad.bfloat16()
+            opt = D.FusedSGD(ps, lr=0.1, momentum=0.9, max_grad_norm=0.5)
+            opt.step()
+            opt.step()
+            torch.cuda.synchronize()
+            res.append(([p.detach().clone() for p in ps], opt.last_grad_norm.clone()))
+    finally:
+        O.CLIP_FUSED = True
+    for x, y in zip(res[0][0], res[1][0]):
+        assert torch.equal(x, y)
+    assert torch.equal(res[0][1], res[1][1])

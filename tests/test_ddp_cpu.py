@@ -300,6 +300,48 @@ def test_find_unused_parameters_used_on_another_rank():
     _run(_unused_across_ranks, 2)
 
 
+def _unused_bf16_buckets(rank, ws):
+    """with bf16 buckets, the grad created for a parameter
+    unused on this rank keeps the parameter's dtype (fp32; torch refuses a
+    grad of another dtype), equals bit for bit the grad the using rank
+    unpacked from the same bucket, and the fused AMP non-finite check covers
+    it — an inf in rank 0's `extra` grad flags found_inf on rank 1 as well, so
+    both ranks take the same skip decision."""
+    import distributed_training_amd as D
+
+    torch.manual_seed(0)
+    model = _Branchy()
+    ddp = D.DistributedDataParallel(model, find_unused_parameters=True, bucket_dtype=torch.bfloat16)
+    found = torch.zeros(1)
+    ddp.set_found_inf_target(found)
+    names = [n for n, _ in model.named_parameters()]
+    ix = names.index("extra.weight")
+    g = torch.Generator().manual_seed(1234 + rank)
+    for it in range(3):
+        for p in model.parameters():
+            p.grad = None
+        x = torch.rand(4, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        loss = torch.nn.functional.cross_entropy(ddp(x, rank == 0), y)
+        if it == 2 and rank == 0:
+            model.extra.weight.register_hook(lambda gr: gr.index_fill(0, torch.tensor([0]), float("inf")))
+        loss.backward()
+        grads = [None if p.grad is None else p.grad for p in model.parameters()]
+        assert all(gr is None or gr.dtype == torch.float32 for gr in grads)
+        w = grads[ix].clone()
+        allw = [torch.zeros_like(w) for _ in range(ws)]
+        dist.all_gather(allw, w)
+        if it < 2:
+            assert torch.equal(allw[0], allw[1]), f"iter {it}: unused rank's grad != using rank's"
+            assert found.item() == 0.0
+        else:
+            assert found.item() == 1.0, f"rank {rank}: the non-finite averaged grad was not flagged"
+
+
+def test_find_unused_parameters_bf16_buckets_and_amp_check():
+    _run(_unused_bf16_buckets, 2)
+
+
 def _unused_after_no_sync(rank, ws):
     """find_unused_parameters + no_sync: a parameter used only in an
     accumulation (no_sync) backward on one rank counts as used for the next

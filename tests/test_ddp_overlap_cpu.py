@@ -110,3 +110,72 @@ def test_overlapped_optimizer_matches_explicit_step_and_torch(kind):
 
 def test_overlapped_optimizer_contract():
     _run(_contract, 2)
+
+
+class _Branchy(nn.Module):
+    """A trunk plus three heads: head a is used on rank 0, head b on rank 1,
+    head c on no rank (find_unused_parameters with rank-dependent usage)."""
+
+    def __init__(self):
+        super().__init__()
+        self.trunk = nn.Linear(12, 16)
+        self.a = nn.Linear(16, 5)
+        self.b = nn.Linear(16, 5)
+        self.c = nn.Linear(16, 5)
+
+    def forward(self, x, which):
+        h = torch.relu(self.trunk(x))
+        return self.a(h) if which == 0 else self.b(h)
+
+
+def _unused_train(rank, kind, impl, bucket_cap_mb):
+    import distributed_training_amd as D
+
+    torch.manual_seed(0)
+    model = _Branchy()
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-2) if kind == "sgd" else dict(lr=1e-2, weight_decay=1e-2)
+    cls = torch.optim.SGD if kind == "sgd" else torch.optim.AdamW
+    if impl == "torch":
+        ddp = torch.nn.parallel.DistributedDataParallel(model, find_unused_parameters=True,
+                                                        bucket_cap_mb=bucket_cap_mb)
+    else:
+        ddp = D.DistributedDataParallel(model, find_unused_parameters=True, bucket_cap_mb=bucket_cap_mb)
+    ddp._register_fused_optim(cls, **kw)
+    g = torch.Generator().manual_seed(77 + rank)
+    grads = []
+    for step in range(3):
+        x = torch.randn(6, 12, generator=g)
+        ddp(x, rank % 2).square().mean().backward()
+        grads.append([None if p.grad is None else p.grad.clone() for p in model.parameters()])
+        for p in model.parameters():
+            p.grad = None
+    return [p.detach().clone() for p in model.parameters()], grads
+
+
+def _unused_compare(rank, ws, kind, bucket_cap_mb):
+    ref, ref_g = _unused_train(rank, kind, "torch", bucket_cap_mb)
+    got, got_g = _unused_train(rank, kind, "libgsync", bucket_cap_mb)
+    w0 = _Branchy()
+    names = [n for n, _ in w0.named_parameters()]
+    tol = dict(rtol=1e-6, atol=1e-7) if kind == "sgd" else dict(rtol=1e-6, atol=1e-6)
+    for n, a, b in zip(names, ref, got):
+        torch.testing.assert_close(b, a, **tol, msg=lambda m: f"{kind} {n} vs torch overlap: {m}")
+    # the never-used head moved (weight decay + momentum on zero grads), as torch's
+    torch.manual_seed(0)
+    init = dict(_Branchy().named_parameters())
+    assert not torch.equal(got[names.index("c.weight")], init["c.weight"].detach())
+    for step, (gr, gg) in enumerate(zip(ref_g, got_g)):
+        for n, a, b in zip(names, gr, gg):
+            assert (a is None) == (b is None), f"step {step} {n}: grad presence differs from torch"
+            if a is not None:
+                torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adamw"])
+@pytest.mark.parametrize("bucket_cap_mb", [None, 0.0005])
+def test_overlapped_optimizer_with_rank_dependent_unused_parameters(kind, bucket_cap_mb):
+    """a parameter unused on this rank but used on another —
+    and one unused everywhere — must be stepped by the overlapped optimizer on
+    every rank, as torch's _hook_then_optimizer steps every bucket parameter
+    with bucket.gradients()."""
+    _run(_unused_compare, 2, kind, bucket_cap_mb)

@@ -105,6 +105,35 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     _check_line(lines[0], 2)
     assert "rehearsal" in lines[0]["config"]
     assert lines[0]["parity"]["collective"] == "gloo"
+    _check_policy_ab(lines[0], 2)
+
+
+def _check_policy_ab(d, n):
+    """The bucket-policy A/B the driver's N>1 run carries (DESIGN §8's rule
+    decides row N1 from it): every variant timed, parity-checked, with its tail."""
+    ab = d["bucket_policy_ab"]
+    assert set(ab["variants"]) == {"torch", "xgmi", "last_bucket_cap_1MiB", "torch_again"}
+    for name, r in ab["variants"].items():
+        assert r["images_per_sec"] > 0 and r["ms_per_step"] > 0, name
+        assert r["parity"]["ok"] is True and r["parity"]["world"] == n, (name, r["parity"])
+        assert r["tail_split_ms"] is None or r["tail_split_ms"]["total"] > 0
+    assert ab["decision"] in ab["variants"]
+    assert "rule" in ab and ab["torch_mean_images_per_sec"] > 0
+    # the tail split caps the last bucket at 1 MiB: one more bucket than the torch layout
+    assert len(ab["variants"]["last_bucket_cap_1MiB"]["bucket_bytes"]) >= len(ab["variants"]["torch"]["bucket_bytes"])
+    if n > 1:
+        assert ab["variants"]["xgmi"]["xgmi_calibration"]["bus_GBps"] > 0
+
+
+def test_bench_policy_ab_n1_rccl(cuda_device):
+    """The same A/B forced on at N=1 over libgsync's RCCL communicator (the
+    comm-side code of the driver's run: re-wrapping, close(), the standalone leg)."""
+    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1", "--policy-ab", "1", "--kernel-rates", "0"]
+                       + SMALL, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _json_lines(p.stdout)[0]
+    _check_policy_ab(d, 1)
+    assert d["bucket_policy_ab"]["variants"]["torch"]["parity"]["collective"] == "rccl(libgsync)"
 
 
 def test_bench_colossal_engine(cuda_device):
