@@ -176,7 +176,8 @@ class _FusedBase(torch.optim.Optimizer):
             return self.grad_scale
         buf = self._clip_buf.get(device)
         if buf is None:
-            buf = torch.zeros(3, dtype=torch.float32, device=device)
+            # [published Σg², coef, norm | accumulated raw Σg² (several plans)]
+            buf = torch.zeros(4, dtype=torch.float32, device=device)
             self._clip_buf[device] = buf
         sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
         self.last_grad_norm = norm
@@ -184,13 +185,16 @@ class _FusedBase(torch.optim.Optimizer):
             if len(all_plans) == 1:
                 plan, gdt = all_plans[0]
                 plan.sqnorm_partial(1, gdt)
-                plan.set_clip(float(max_norm), 1e-6, None, out=buf)
+                plan.set_clip(float(max_norm), 1e-6, None, out=buf[0:3])
                 plan._clip_on = True
             else:
+                # the raw sum lives apart from the published triple: every update
+                # launch reads it while workgroup 0 of each writes the (scaled) Σg²
+                raw = buf[3:4]
                 for i, (plan, gdt) in enumerate(all_plans):
-                    plan.sqnorm(1, gdt, sq, accumulate=i > 0)
+                    plan.sqnorm(1, gdt, raw, accumulate=i > 0)
                 for plan, _ in all_plans:
-                    plan.set_clip(float(max_norm), 1e-6, sq, out=buf)
+                    plan.set_clip(float(max_norm), 1e-6, raw, out=buf[0:3])
                     plan._clip_on = True
             return self.grad_scale  # the kernels fold it into the coefficient
         for plan, _ in all_plans:
@@ -393,6 +397,7 @@ class FusedAdam(_FusedBase):
             buckets = {}
             by_cohort: dict = {}
             h = None
+            live = []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -408,6 +413,11 @@ class FusedAdam(_FusedBase):
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                live.append(p)
+            # every state of this step exists before cohorts are formed: parameters
+            # whose state starts together share one cohort (one counter, one plan)
+            for p in live:
+                st = self.state[p]
                 if cap:
                     if h is None:
                         h = self._group_hyper(gi, group, p.device)

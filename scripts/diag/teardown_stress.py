@@ -24,8 +24,15 @@ def worker(fn_name, rank, ws, port):
     from tests import test_ddp_cpu as T
     from tests._dist_util import init_pg
 
+    import torch
+    import torch.distributed as dist
+
     init_pg("gloo", rank, ws, port)
+    torch.set_num_threads(max(1, 8 // ws))
     getattr(T, fn_name)(rank, ws)
+    if os.environ.get("NO_DESTROY", "0") == "0":  # as tests/test_ddp_cpu.py:_wrap
+        dist.barrier()
+        dist.destroy_process_group()
     # normal interpreter exit from here (atexit, module teardown, static destructors)
 
 

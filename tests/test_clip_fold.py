@@ -83,6 +83,51 @@ def test_folded_clip_skipped_step_cpu():
     assert torch.equal(fused[0][0], _params(dev)[0].detach())  # nothing moved
 
 
+@pytest.mark.parametrize("opt_cls,kw", CASES)
+@pytest.mark.parametrize("gscale", [None, 0.5, 0.125])
+@pytest.mark.parametrize("found_inf", [0.0, 1.0])
+def test_folded_clip_amp_device_state_cpu(opt_cls, kw, gscale, found_inf):
+    """The AMP path (found_inf set: device step counters / first-step flags)
+    with an unscale multiplier: the folded clip equals the separate one."""
+    dev = torch.device("cpu")
+    _assert_same(_run(dev, True, opt_cls, kw, gscale, found_inf=found_inf),
+                 _run(dev, False, opt_cls, kw, gscale, found_inf=found_inf))
+
+
+def test_folded_clip_several_plans_cpu():
+    """Two grad dtypes -> two plans: Σg² accumulated into one scalar that every
+    update launch reads while each publishes the scaled Σg² (kept apart)."""
+    dev = torch.device("cpu")
+    res = []
+    for fused in (True, False):
+        O.CLIP_FUSED = fused
+        try:
+            ps = _params(dev)
+            ps[1].grad_dtype = None  # torch 2.10: a grad of another dtype needs this
+            ps[1].grad = ps[1].grad.bfloat16()
+            opt = D.FusedSGD(ps, lr=0.1, momentum=0.9, max_grad_norm=1.0)
+            opt.grad_scale = torch.tensor([0.25])
+            for _ in range(2):
+                opt.step()
+            res.append(([p.detach().clone() for p in ps], opt.last_grad_norm.clone()))
+        finally:
+            O.CLIP_FUSED = True
+    for x, y in zip(res[0][0], res[1][0]):
+        assert torch.equal(x, y)
+    assert torch.equal(res[0][1], res[1][1])
+
+
+def test_amp_adam_first_step_one_cohort_cpu():
+    """Parameters whose Adam state starts in the same step share one device
+    step counter and one update plan (they got one each: a launch per tensor)."""
+    ps = _params(torch.device("cpu"))
+    opt = D.FusedAdam(ps, lr=1e-3)
+    opt.found_inf = torch.zeros(1)
+    opt.step()
+    assert len(list(opt._plans.plans())) == 1
+    assert len({id(opt.state[p]["step"]) for p in ps}) == 1
+
+
 def test_plan_clip_needs_partial_first():
     plan = D.multi_tensor.TensorListPlan([8], torch.device("cpu"), task_units=0)
     p, g, b = torch.zeros(8), torch.ones(8), torch.zeros(8)
@@ -112,10 +157,12 @@ def test_folded_clip_equals_separate_path_gpu(opt_cls, kw, gscale):
 
 
 @pytest.mark.gpu
-def test_folded_clip_skipped_step_gpu():
+@pytest.mark.parametrize("opt_cls,kw", CASES)
+@pytest.mark.parametrize("found_inf", [0.0, 1.0])
+def test_folded_clip_amp_device_state_gpu(opt_cls, kw, found_inf):
     dev = torch.device("cuda", 0)
-    _assert_same(_run(dev, True, D.FusedAdam, dict(lr=1e-3), 0.5, found_inf=1.0),
-                 _run(dev, False, D.FusedAdam, dict(lr=1e-3), 0.5, found_inf=1.0))
+    _assert_same(_run(dev, True, opt_cls, kw, 0.5, found_inf=found_inf),
+                 _run(dev, False, opt_cls, kw, 0.5, found_inf=found_inf))
 
 
 @pytest.mark.gpu
@@ -134,6 +181,7 @@ def test_folded_clip_large_plan_gpu(mixed):
             for p in ps:
                 p.grad = torch.randn(p.shape, device=dev, generator=g) * 0.01
             if mixed:
+                ps[1].grad_dtype = None  # torch 2.10: a grad of another dtype needs this
                 ps[1].grad = ps[1].grad.bfloat16()
             opt = D.FusedSGD(ps, lr=0.1, momentum=0.9, max_grad_norm=0.5)
             opt.step()
