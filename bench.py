@@ -187,7 +187,7 @@ def grad_sync_kernel_rates(params, dev, iters=20):
             fn()
         ts = p_.timer_read()
         p_.timer_enable(0)
-        return sum(ts) / len(ts)
+        return sum(ts) / iters  # per call: every launch the call makes counts
 
     rows = {}
     for name, nbytes, fn in (
@@ -207,6 +207,22 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     up.set_ptrs(2, bs)
     ms = rate(lambda: up.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False), up)
     rows["sgd_momentum_wd"] = {"alg_bytes": 20 * n, "avg_ms": ms, "GBps": 20 * n / (ms * 1e-3) / 1e9}
+    # the clip path as the folded clip runs it (DeepSpeed gradient_clipping,
+    # R:resnet/deepspeed/deepspeed_train.py:195): Σg² partial sums, then the update
+    # whose workgroups form the coefficient from them — both launches timed
+    ms = rate(lambda: up.sqnorm_partial(1, torch.float32), up)
+    rows["sqnorm_partial_f32"] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9}
+    clip_out = torch.zeros(3, device=dev)
+
+    def clipped_sgd():
+        up.sqnorm_partial(1, torch.float32)
+        up.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)
+
+    up.set_clip(1.0, 1e-6, None, out=clip_out)
+    ms = rate(clipped_sgd, up)
+    up.set_clip(None)
+    rows["clip_path_sgd"] = {"alg_bytes": 24 * n, "avg_ms": ms, "GBps": 24 * n / (ms * 1e-3) / 1e9,
+                             "launches": "sqnorm_partial + clipped sgd"}
     up.set_ptrs(3, vs)
     ms = rate(lambda: up.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5), up)
     rows["adam"] = {"alg_bytes": 28 * n, "avg_ms": ms, "GBps": 28 * n / (ms * 1e-3) / 1e9}

@@ -199,6 +199,35 @@ def available() -> bool:
         return False
 
 
+HOOK_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "_gshook.so")
+_hook_mod = None
+_hook_error: str | None = None
+
+
+def hook_module():
+    """The _gshook extension (C++ DDP gradient hooks, csrc/gs_torch_hook.cpp),
+    or None when it is not built — DDP then keeps its Python hooks, which call
+    the same library.  It links lib/libgsync.so itself, so a GSYNC_LIB variant
+    (a different library instance) disables it."""
+    global _hook_mod, _hook_error
+    if _hook_mod is not None or _hook_error is not None:
+        return _hook_mod
+    lib()  # libgsync first: _gshook resolves its symbols from the loaded copy
+    if os.path.realpath(LIB_PATH) != os.path.realpath(os.path.join(os.path.dirname(HOOK_PATH), "libgsync.so")):
+        _hook_error = f"GSYNC_LIB={LIB_PATH} is not the library _gshook links"
+        return None
+    if not os.path.exists(HOOK_PATH):
+        _hook_error = f"{HOOK_PATH} is not built"
+        return None
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_gshook", HOOK_PATH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    _hook_mod = mod
+    return mod
+
+
 def check(rc: int, what: str = "") -> int:
     if rc < 0:
         msg = lib().gs_last_error().decode(errors="replace")
@@ -239,3 +268,37 @@ def stream_ptr(device: torch.device) -> int | None:
     if device.type != "cuda":
         return None
     return torch.cuda.current_stream(device).cuda_stream
+
+
+# ---- capture-safe destruction.  Freeing a plan / bucketer / communicator
+# synchronises streams and frees device memory, which is illegal while a
+# stream of this thread records a hipGraph (the recording is invalidated and
+# capture_end faults).  Python's garbage collector can run at any allocation,
+# including inside a capture (an old DDP / optimizer in a reference cycle): a
+# destroy requested then is parked and run at the next safe point.
+_deferred: list = []
+
+
+def _capturing() -> bool:
+    try:
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    except Exception:  # pragma: no cover - no device / interpreter teardown
+        return False
+
+
+def destroy(fn_name: str, handle) -> None:
+    """lib().<fn_name>(handle) now, or after the current capture ends."""
+    if _capturing():
+        _deferred.append((fn_name, handle))
+        return
+    getattr(lib(), fn_name)(handle)
+
+
+def flush_deferred() -> None:
+    """Run the destroys parked during a capture (no-op while still capturing)."""
+    if not _deferred or _capturing():
+        return
+    while _deferred:
+        fn_name, h = _deferred.pop(0)
+        getattr(lib(), fn_name)(h)
+

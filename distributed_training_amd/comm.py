@@ -44,6 +44,12 @@ class Communicator:
         torch.cuda.set_device(device)
         L.check(lib.gs_comm_create(self.rank, self.world, uid, device.index, ctypes.byref(h)), "gs_comm_create")
         self.handle = h
+        import weakref
+
+        # bucketers built on this communicator: closed first when it closes (they
+        # synchronise its stream at destruction — a freed communicator there was a
+        # use-after-free once the comm went before a bucketer still awaiting GC)
+        self._users = weakref.WeakSet()
         s = ctypes.c_void_p()
         L.check(lib.gs_comm_stream(h, ctypes.byref(s)), "gs_comm_stream")
         self.stream_ptr = s.value
@@ -96,10 +102,16 @@ class Communicator:
             return uid
         return bytes(store.get(key))
 
+    def add_user(self, obj):
+        """`obj` (with a close()) holds library objects bound to this communicator."""
+        self._users.add(obj)
+
     def close(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
-            L.lib().gs_comm_destroy(h)
+            for u in list(getattr(self, "_users", ())):
+                u.close()
+            L.destroy("gs_comm_destroy", h)
             self.handle = None
 
     def abort(self):

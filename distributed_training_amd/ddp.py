@@ -183,7 +183,9 @@ class _Bucketer:
     """Python owner of one gs_bucketer + its torch-allocated bucket storage."""
 
     def __init__(self, ddp, buckets, flags):
-        self.ddp = ddp
+        import weakref
+
+        self._ddp_ref = weakref.ref(ddp)  # no DDP <-> bucketer cycle: freed when the DDP goes
         params = ddp._params
         self.buckets = buckets
         self.flags = flags
@@ -206,6 +208,8 @@ class _Bucketer:
             "gs_bucketer_create",
         )
         self.handle = h
+        if ddp._comm is not None:
+            ddp._comm.add_user(self)
         self.buffers = []
         for b in range(len(buckets)):
             if any(params[i].dtype != self.grad_dtypes[b] for i in buckets[b]):
@@ -231,6 +235,10 @@ class _Bucketer:
         self._mark = L.lib().gs_bucketer_mark_ready
         self._n_ready_ref = ctypes.byref(self._n_ready)
 
+    @property
+    def ddp(self):
+        return self._ddp_ref()
+
     def bucket_view(self, i):
         b, off = self.loc[i]
         p = self.ddp._params[i]
@@ -244,7 +252,10 @@ class _Bucketer:
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
-            L.lib().gs_bucketer_destroy(self.handle)
+            nat = getattr(self.ddp, "_native", None)
+            if nat is not None:
+                nat.set_bucketer(0, 0)  # the C++ hooks must not reach a destroyed bucketer
+            L.destroy("gs_bucketer_destroy", self.handle)
             self.handle = None
 
     def __del__(self):
@@ -252,6 +263,27 @@ class _Bucketer:
             self.close()
         except Exception:  # pragma: no cover
             pass
+
+
+def _make_native_hooks(ddp):
+    """The C++ hook object for `ddp` (None when GSYNC_NATIVE_HOOK=0 or the
+    extension is not built).  Its end-of-backward callback holds the DDP
+    weakly (the hooks live as long as the DDP, not the other way round)."""
+    if os.environ.get("GSYNC_NATIVE_HOOK", "1") == "0":
+        return None
+    mod = L.hook_module()
+    if mod is None:
+        return None
+    import weakref
+
+    ref = weakref.ref(ddp)
+
+    def on_finalize():
+        d = ref()
+        if d is not None:
+            d._native_finalized()
+
+    return mod.Hooks(ddp._params, ddp._dev_index, on_finalize)
 
 
 class DistributedDataParallel(nn.Module):
@@ -376,8 +408,15 @@ class DistributedDataParallel(nn.Module):
         self._ready_now: list = []
         self._overlap: dict | None = None  # _register_fused_optim state
         self._param_index = {id(p): i for i, p in enumerate(self._params)}
-        self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
-                              for i, p in enumerate(self._params)]
+        self._hook_handles = []
+        # C++ gradient hooks (_gshook: AccumulateGrad post-hooks calling
+        # gs_bucketer_mark_ready, as torch's Reducer) on the fast path; the Python
+        # hooks below serve every other configuration.  _set_native switches.
+        self._native = _make_native_hooks(self) if self.device.type == "cuda" else None
+        self._native_on = False
+        if self._native is not None:
+            self._native.set_bucketer(self._bucketer.handle.value, len(self._bucketer.buckets))
+        self._set_native(self._native_ok())
 
     # ------------------------------------------------------------------ setup
     def _flags(self):
@@ -406,7 +445,46 @@ class DistributedDataParallel(nn.Module):
             L.check(L.lib().gs_bucketer_set_timeline(b.handle, lvl), "gs_bucketer_set_timeline")
         if getattr(self, "_overlap", None) is not None:
             self._overlap["per_bucket"] = {}  # bucket membership changed
+        if getattr(self, "_native", None) is not None:
+            self._native.set_bucketer(b.handle.value, len(buckets))
         return b
+
+    # ---- which hooks run: C++ (_gshook) on the fast path, Python otherwise
+    def _native_ok(self) -> bool:
+        return (self._native is not None and bool(self._bucketer.flags & L.GS_BKT_AUTO_COLLECTIVE)
+                and not self.find_unused_parameters and self._overlap is None and self._comm_hook is None
+                and self._capture_local is None)
+
+    def _set_native(self, on: bool):
+        if on:
+            for h in self._hook_handles:
+                h.remove()
+            self._hook_handles = []
+            self._native.attach()
+        else:
+            if self._native is not None:
+                self._native.detach()
+            if not self._hook_handles:
+                self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                                      for i, p in enumerate(self._params)]
+        self._native_on = on
+
+    def _native_finalized(self):
+        """End of a backward whose hooks and gs_bucketer_finalize ran in C++:
+        the Python side of _finalize_backward (once per backward)."""
+        if self._record_order:
+            self._ready_order = list(self._native.order())
+        self._found_inf_valid = self._found_inf_target is not None
+        if self.gradient_as_bucket_view:
+            b = self._bucketer
+            for i, p in enumerate(self._params):
+                if p.grad is not None:
+                    view = b.bucket_view(i)
+                    if p.grad.data_ptr() != view.data_ptr():
+                        p.grad = view
+        self._in_backward = False
+        self._finalize_queued = False
+        self._num_iterations += 1
 
     def _calib_allreduce(self, nbytes: int, iters: int = 4) -> float:
         """Median time (s, MAX over ranks) of one SUM all-reduce of nbytes of
@@ -584,6 +662,7 @@ class DistributedDataParallel(nn.Module):
                 and len(self._module_buffers()) != 0)
 
     def forward(self, *inputs, **kwargs):
+        L.flush_deferred()
         if self._comm is not None:
             self._comm.check()  # watchdog / RCCL async error surfaces here, like ProcessGroupNCCL's
         grad_sync = torch.is_grad_enabled() and self.require_backward_grad_sync
@@ -605,6 +684,11 @@ class DistributedDataParallel(nn.Module):
         return output
 
     def _prepare_for_backward(self):
+        want = self._native_ok()
+        if want != self._native_on:
+            self._set_native(want)
+        if self._native_on and self._in_backward and self._native.finalize_queued():
+            self._finalize_queued = True
         if self._in_backward and self._finalize_queued:
             raise RuntimeError(
                 "Expected to have finished reduction in the prior iteration before starting a new one. "
@@ -622,6 +706,8 @@ class DistributedDataParallel(nn.Module):
         self._ready_now = []
         if self._record_order:
             self._ready_order = []
+        if self._native_on:
+            self._native.prepare(self._record_order)
 
     @contextmanager
     def no_sync(self):
@@ -1101,6 +1187,9 @@ class DistributedDataParallel(nn.Module):
             except Exception:  # pragma: no cover
                 pass
         self._hook_handles = []
+        if getattr(self, "_native", None) is not None:
+            self._native.detach()
+            self._native_on = False
         b = getattr(self, "_bucketer", None)
         if b is not None:
             if self.gradient_as_bucket_view:
@@ -1115,6 +1204,9 @@ class DistributedDataParallel(nn.Module):
                 h.remove()
             except Exception:  # pragma: no cover
                 pass
+        nat = getattr(self, "_native", None)
+        if nat is not None:
+            nat.detach()
 
 
 DDP = DistributedDataParallel

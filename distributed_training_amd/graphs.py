@@ -114,6 +114,7 @@ class CapturedStep:
                 self._out = self.step_fn(*self._inputs)
         finally:
             L.check(L.lib().gs_watchdog_pause(0), "gs_watchdog_pause")
+            L.flush_deferred()  # destroys the garbage collector requested mid-recording
         self.graph = g
         self.captures += 1
 

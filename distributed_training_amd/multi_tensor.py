@@ -61,7 +61,7 @@ class TensorListPlan:
         h = getattr(self, "handle", None)
         if h is not None and h.value:
             try:
-                L.lib().gs_plan_destroy(h)
+                L.destroy("gs_plan_destroy", h)
             except Exception:  # pragma: no cover - interpreter shutdown
                 pass
             self.handle = None

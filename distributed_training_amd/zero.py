@@ -160,6 +160,8 @@ class ZeroDataParallel:
             L.gs_dtype(self.dtype), BUCKET_ALIGN_ELEMS, float(self.world), flags, ctypes.byref(h)),
             "gs_bucketer_create")
         self.handle = h
+        if self._comm is not None:
+            self._comm.add_user(self)
         self._ready = (ctypes.c_int32 * max(1, len(self.buckets)))()
         self._n_ready = ctypes.c_int32()
         q = self.world * BUCKET_ALIGN_ELEMS
@@ -453,7 +455,7 @@ class ZeroDataParallel:
         for h in self._hooks:
             h.remove()
         if getattr(self, "handle", None) is not None and self.handle.value:
-            L.lib().gs_bucketer_destroy(self.handle)
+            L.destroy("gs_bucketer_destroy", self.handle)
             self.handle = None
 
 

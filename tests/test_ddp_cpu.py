@@ -53,20 +53,6 @@ def _wrap(fn, rank, ws, port, errq, *args):
 
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
-    _exit_ok()
-
-
-def _exit_ok():
-    """End a worker that finished cleanly without interpreter finalisation:
-    torch's gloo teardown at exit occasionally aborts ("terminate called
-    without an active exception", exit -6, about 1 run in 40 under load) after
-    every check has passed; the result is already reported, so skip it."""
-    import os
-    import sys
-
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(0)
 
 
 def _golden_run(rank, ws, name, use_torch_opt, hook):
@@ -182,7 +168,11 @@ def _side_by_side(rank, ws, mode):
         for (na, pa), (nb, pb) in zip(a.module.named_parameters(), b.module.named_parameters()):
             assert (pa.grad is None) == (pb.grad is None), na
             if pa.grad is not None:
-                assert torch.equal(pa.grad, pb.grad), f"{mode} it {it} {na}"
+                if ws <= 2:
+                    assert torch.equal(pa.grad, pb.grad), f"{mode} it {it} {na}"
+                else:  # gloo's ring sums in a chunk order that depends on the bucket layout
+                    torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-5, atol=1e-6,
+                                               msg=f"{mode} it {it} {na}")
         if mode == "view":
             for p in a.module.parameters():
                 p.grad.zero_()
@@ -197,6 +187,13 @@ def _side_by_side(rank, ws, mode):
 @pytest.mark.parametrize("mode", ["no_sync", "view", "small_buckets", "find_unused"])
 def test_side_by_side_with_torch_ddp(mode):
     _run(_side_by_side, 2, mode)
+
+
+def test_side_by_side_ws4_many_buckets_rebuild():
+    """4 ranks, more than 3 buckets, the rebuild after the first iteration and
+    the rank-0 layout broadcast (Reducer::sync_bucket_indices): the step-1 code
+    of the 4-rank rehearsal against torch's DDP."""
+    _run(_side_by_side, 4, "small_buckets")
 
 
 def _state_dict_keys(rank, ws):

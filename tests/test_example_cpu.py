@@ -17,7 +17,6 @@ import torch.multiprocessing as mp
 import torch.nn as nn
 
 from tests._dist_util import free_port
-from tests.test_ddp_cpu import _exit_ok
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -60,7 +59,6 @@ def _reference(rank, ws, port, steps, batch, n, q):
         out.update(grads)
         q.put(out)
     dist.destroy_process_group()
-    _exit_ok()
 
 
 def _mine(rank, ws, port, steps, batch, n, q):
@@ -74,7 +72,6 @@ def _mine(rank, ws, port, steps, batch, n, q):
     ex = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ex)
     ex.ddp(rank, ws, 1, 1e-3 * ws, batch, "cpu", max_steps=steps, synthetic_n=n, port=port, result=q)
-    _exit_ok()
 
 
 def _run(fn, ws, steps, batch, n):
