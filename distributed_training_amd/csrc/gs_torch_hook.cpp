@@ -72,6 +72,8 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
       : params_(std::move(params)), device_(device), on_finalize_(on_finalize.release().ptr()) {
     dense_strides_.resize(params_.size());
     dense_seen_.assign(params_.size(), 0);
+    accs_.resize(params_.size());
+    keys_.assign(params_.size(), 0);
   }
   ~Hooks() {
     detach();
@@ -81,24 +83,23 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     if (on_finalize_ && Py_IsInitialized() && PyGILState_Check()) Py_DECREF(on_finalize_);
   }
 
-  void attach() {
-    if (!keys_.empty()) return;
-    for (size_t i = 0; i < params_.size(); ++i) {
-      // the accumulator is held weakly by the variable: keep it alive, as the Reducer does
-      auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
-      if (!acc) throw std::runtime_error("_gshook: parameter " + std::to_string(i) + " has no grad accumulator");
-      keys_.push_back(acc->add_post_hook(std::make_unique<MarkReady>(this, static_cast<int>(i))));
-      accs_.push_back(std::move(acc));
+  // The hooks go on the AccumulateGrad nodes of each synchronising forward's
+  // graph (arm(), from prepare()), not on nodes created and pinned here: an
+  // AccumulateGrad runs on the stream that was current when it was created, so
+  // a node pinned at wrap time would accumulate on that stream even inside a
+  // later hipGraph capture on another one.  The variable holds its node
+  // weakly; the graph owns it and frees it, hook included, after backward.
+  void attach() { active_ = true; }
+
+  void detach() {
+    active_ = false;
+    for (size_t i = 0; i < accs_.size(); ++i) {
+      if (auto a = accs_[i].lock()) a->del_post_hook(keys_[i]);
+      accs_[i].reset();
     }
   }
 
-  void detach() {
-    for (size_t i = 0; i < keys_.size(); ++i) accs_[i]->del_post_hook(keys_[i]);
-    keys_.clear();
-    accs_.clear();
-  }
-
-  bool attached() const { return !keys_.empty(); }
+  bool attached() const { return active_; }
 
   void set_bucketer(uintptr_t handle, int n_buckets) {
     b_ = reinterpret_cast<gs_bucketer*>(handle);
@@ -111,6 +112,19 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     finalize_queued_ = false;
     record_order_ = record_order;
     if (record_order) order_.clear();
+    if (active_) arm();
+  }
+
+  // one post-hook on each parameter's AccumulateGrad in the graph just built
+  // (a node that outlived its graph, e.g. retain_graph, keeps its one hook)
+  void arm() {
+    for (size_t i = 0; i < params_.size(); ++i) {
+      auto a = torch::autograd::impl::try_get_grad_accumulator(params_[i]);
+      if (!a) continue;  // not in this graph
+      if (accs_[i].lock() == a) continue;
+      keys_[i] = a->add_post_hook(std::make_unique<MarkReady>(this, static_cast<int>(i)));
+      accs_[i] = a;
+    }
   }
 
   void on_grad(int i) {
@@ -179,8 +193,9 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
   std::vector<at::Tensor> params_;
   int device_;
   PyObject* on_finalize_;  // strong reference (see the constructor)
-  std::vector<std::shared_ptr<Node>> accs_;
+  std::vector<std::weak_ptr<Node>> accs_;  // the node each hook is on (owned by its graph)
   std::vector<uintptr_t> keys_;
+  bool active_ = false;
   std::vector<std::vector<int64_t>> dense_strides_;
   std::vector<char> dense_seen_;
   gs_bucketer* b_ = nullptr;
