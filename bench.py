@@ -182,7 +182,7 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     def rate(fn, p_):
         for _ in range(3):
             fn()
-        p_.timer_enable(iters)
+        p_.timer_enable(4 * iters)  # room for every launch of a multi-launch call (the ring keeps the last)
         for _ in range(iters):
             fn()
         ts = p_.timer_read()

@@ -144,7 +144,7 @@ constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too 
 #define GS_G_PACK 1     // fp32 bucket
 #endif
 #ifndef GS_G_PACK16
-#define GS_G_PACK16 2   // 16-bit bucket
+#define GS_G_PACK16 8   // 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
 #endif
 #ifndef GS_G_UNPACK
 #define GS_G_UNPACK 2

@@ -316,10 +316,15 @@ class DistributedDataParallel(nn.Module):
         self.bucket_bytes_cap = int((25 if bucket_cap_mb is None else bucket_cap_mb) * 1024 * 1024)
         self.first_bucket_bytes_cap = DEFAULT_FIRST_BUCKET_BYTES if self.bucket_bytes_cap_default else self.bucket_bytes_cap
 
-        # parameters handed to the bucketer: module order, requires_grad, no duplicates
+        # parameters handed to the bucketer: module order, requires_grad, no duplicates,
+        # minus the names _set_params_and_buffers_to_ignore_for_model listed (torch's
+        # ``parameters_to_ignore``: neither synchronised nor broadcast)
+        self.parameters_to_ignore = set(getattr(module, "_ddp_params_and_buffers_to_ignore", ()))
         seen = set()
         self._params, self._param_names = [], []
         for name, p in module.named_parameters():
+            if name in self.parameters_to_ignore:
+                continue
             if p.requires_grad and id(p) not in seen:
                 seen.add(id(p))
                 self._params.append(p)
@@ -563,7 +568,8 @@ class DistributedDataParallel(nn.Module):
         # walking the module tree every forward costs ~0.3 ms of host time a step
         bufs = getattr(self, "_modules_buffers", None)
         if bufs is None:
-            bufs = self._modules_buffers = list(self.module.buffers())
+            bufs = self._modules_buffers = [b for n, b in self.module.named_buffers()
+                                            if n not in self.parameters_to_ignore]
         return bufs
 
     def _broadcast_tensors(self, tensors):
@@ -607,7 +613,9 @@ class DistributedDataParallel(nn.Module):
         Every parameter, frozen ones included (torch's ``module_states`` walks
         ``named_parameters()`` without a requires_grad filter)."""
         seen, params = set(), []
-        for p in self.module.parameters():
+        for n, p in self.module.named_parameters():
+            if n in self.parameters_to_ignore:
+                continue
             if id(p) not in seen:
                 seen.add(id(p))
                 params.append(p.detach())
@@ -1173,6 +1181,19 @@ class DistributedDataParallel(nn.Module):
             "num_parameter_tensors": len(self._params),
             "total_parameter_size_bytes": sum(p.numel() * p.element_size() for p in self._params),
         }
+
+    @staticmethod
+    def _set_params_and_buffers_to_ignore_for_model(module, params_and_buffers_to_ignore):
+        """torch's static helper (T:nn/parallel/distributed.py): names (as in
+        ``named_parameters`` / ``named_buffers``) that a DDP wrapping `module`
+        neither synchronises nor broadcasts.  Call before wrapping."""
+        module._ddp_params_and_buffers_to_ignore = params_and_buffers_to_ignore
+        for name, param in module.named_parameters():
+            if name in params_and_buffers_to_ignore:
+                param._ddp_ignored = True
+        for name, buffer in module.named_buffers():
+            if name in params_and_buffers_to_ignore:
+                buffer._ddp_ignored = True
 
     def bucket_indices(self):
         return [list(b) for b in self._bucketer.buckets]

@@ -196,6 +196,40 @@ def test_side_by_side_ws4_many_buckets_rebuild():
     _run(_side_by_side, 4, "small_buckets")
 
 
+def _ignored(rank, ws):
+    """_set_params_and_buffers_to_ignore_for_model: the listed parameter keeps its
+    local grad and its own init, the listed buffer is not broadcast — as torch."""
+    import distributed_training_amd as D
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+
+    torch.manual_seed(1 + rank)  # rank-dependent init: broadcast (or not) shows
+    m1 = _micro()
+    m2 = _micro()
+    m2.load_state_dict(m1.state_dict())
+    ignore = ["fc.weight", "bn1.running_mean"]
+    for m in (m1, m2):
+        D.DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(m, ignore)
+    a = D.DistributedDataParallel(m1, broadcast_buffers=False)
+    b = TDDP(m2, broadcast_buffers=False)
+    assert "fc.weight" not in a._param_names and len(a._params) == len(b._module_parameters)
+    for (n, x), y in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(x, y), n  # the same init broadcast (or kept) as torch
+    g = torch.Generator().manual_seed(9 + rank)
+    for it in range(2):
+        x = torch.rand(3, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (3,), generator=g)
+        for model in (a, b):
+            nn.functional.cross_entropy(model(x), y).backward()
+        for (n, pa), pb in zip(m1.named_parameters(), m2.parameters()):
+            assert torch.equal(pa.grad, pb.grad), f"it {it} {n}"
+        m1.zero_grad()
+        m2.zero_grad()
+
+
+def test_params_and_buffers_to_ignore_match_torch():
+    _run(_ignored, 2)
+
+
 def _state_dict_keys(rank, ws):
     import distributed_training_amd as D
 
