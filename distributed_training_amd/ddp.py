@@ -38,6 +38,7 @@ from typing import Any, Callable
 import torch
 import torch.distributed as dist
 import torch.nn as nn
+from torch.distributed.algorithms.join import Join, Joinable, JoinHook
 
 from . import _lib as L
 from .comm import get_communicator
@@ -286,7 +287,7 @@ def _make_native_hooks(ddp):
     return mod.Hooks(ddp._params, ddp._dev_index, on_finalize)
 
 
-class DistributedDataParallel(nn.Module):
+class DistributedDataParallel(nn.Module, Joinable):
     def __init__(self, module, device_ids=None, output_device=None, dim=0, broadcast_buffers=True,
                  init_sync=True, process_group=None, bucket_cap_mb=None, find_unused_parameters=False,
                  check_reduction=False, gradient_as_bucket_view=False, static_graph=False,
@@ -294,6 +295,7 @@ class DistributedDataParallel(nn.Module):
                  device_mesh=None, skip_all_reduce_unused_params=False, *, bucket_dtype=None,
                  collective: str = "auto", bucket_policy: str = "torch", last_bucket_cap_mb=None):
         super().__init__()
+        Joinable.__init__(self)  # the join config (disabled until a Join context enables it)
         if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
             raise NotImplementedError("delay_all_reduce_named_params is outside the gradient-sync path")
         if mixed_precision is not None or device_mesh is not None:
@@ -572,9 +574,10 @@ class DistributedDataParallel(nn.Module):
                                             if n not in self.parameters_to_ignore]
         return bufs
 
-    def _broadcast_tensors(self, tensors):
-        """Broadcast tensors from rank 0: floating tensors go through the
-        libgsync pack kernel + one broadcast + unpack; others through a cat."""
+    def _broadcast_tensors(self, tensors, root: int = 0):
+        """Broadcast tensors from group rank `root` (0 but under join): floating
+        tensors go through the libgsync pack kernel + one broadcast + unpack;
+        others through a cat."""
         if self.world_size == 1 or not tensors:
             return
         floats = [t for t in tensors if t.is_floating_point() and is_dense(t)]
@@ -586,26 +589,26 @@ class DistributedDataParallel(nn.Module):
             plan = TensorListPlan([t.numel() for t in ts], self.device, align=BUCKET_ALIGN_ELEMS)
             plan.set_ptrs(0, ts)
             flat = torch.zeros(plan.flat_numel, dtype=dt, device=self.device)
-            if self.rank == 0:
+            if self.rank == root:
                 plan.pack(0, dt, flat)
-            self._bcast_flat(flat)
-            if self.rank != 0:
+            self._bcast_flat(flat, root)
+            if self.rank != root:
                 plan.unpack(flat, 0, dt)
         if others:
             flat = torch.cat([t.reshape(-1) for t in others])
-            self._bcast_flat(flat)
-            if self.rank != 0:
+            self._bcast_flat(flat, root)
+            if self.rank != root:
                 off = 0
                 for t in others:
                     t.copy_(flat[off:off + t.numel()].view_as(t))
                     off += t.numel()
 
-    def _bcast_flat(self, flat):
+    def _bcast_flat(self, flat, root: int = 0):
         if self._comm is not None:
-            self._comm.broadcast(flat, root=0, stream=L.stream_ptr(self.device))
+            self._comm.broadcast(flat, root=root, stream=L.stream_ptr(self.device))
         else:
-            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, 0)
-                           if self.process_group is not dist.group.WORLD else 0, group=self.process_group)
+            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, root)
+                           if self.process_group is not dist.group.WORLD else root, group=self.process_group)
 
     @torch.no_grad()
     def _sync_module_states(self):
@@ -622,7 +625,7 @@ class DistributedDataParallel(nn.Module):
         self._broadcast_tensors(params + self._module_buffers())
 
     @torch.no_grad()
-    def _sync_buffers(self):
+    def _sync_buffers(self, root: int = 0):
         """Per-forward BN buffer broadcast (T:nn/parallel/distributed.py:2178-2221):
         one pack launch + one RCCL broadcast + one unpack launch per word size,
         plan cached across steps.  Integer buffers (BN num_batches_tracked,
@@ -650,15 +653,15 @@ class DistributedDataParallel(nn.Module):
         _, plans, others = self._buffers_plan
         for plan, ws, dt, flat in plans:
             plan.set_ptrs(0, ws)
-            if self.rank == 0:
+            if self.rank == root:
                 plan.pack(0, dt, flat)
-            self._bcast_flat(flat)
-            if self.rank != 0:
+            self._bcast_flat(flat, root)
+            if self.rank != root:
                 plan.unpack(flat, 0, dt)
         if others:
             flat = torch.cat([t.reshape(-1) for t in others])
-            self._bcast_flat(flat)
-            if self.rank != 0:
+            self._bcast_flat(flat, root)
+            if self.rank != root:
                 off = 0
                 for t in others:
                     t.copy_(flat[off:off + t.numel()].view_as(t))
@@ -674,10 +677,17 @@ class DistributedDataParallel(nn.Module):
         if self._comm is not None:
             self._comm.check()  # watchdog / RCCL async error surfaces here, like ProcessGroupNCCL's
         grad_sync = torch.is_grad_enabled() and self.require_backward_grad_sync
+        # under ddp.join(): tell the joined ranks this one is still training (their
+        # Join context counts these), as torch's forward does
+        Join.notify_join_context(self)
         if grad_sync:
             self._maybe_rebuild_buckets()
+        joining = self._join_config.enable
         if self._will_sync_module_buffers():
-            self._sync_buffers()
+            # under join rank 0 may have stopped: the highest still-training rank is the source
+            self._sync_buffers(self._find_common_rank(self.rank, True) if joining else 0)
+        if joining:
+            self._check_global_requires_backward_grad_sync(is_joined_rank=False)
         if self.device_ids:
             dev = torch.device(self.device_type, self.device_ids[0])
             inputs = tuple(x.to(dev, non_blocking=True) if isinstance(x, torch.Tensor) else x for x in inputs)
@@ -1182,6 +1192,78 @@ class DistributedDataParallel(nn.Module):
             "total_parameter_size_bytes": sum(p.numel() * p.element_size() for p in self._params),
         }
 
+    # ---- uneven inputs: torch's DDP.join() (T:nn/parallel/distributed.py join /
+    # _DDPJoinHook, T:distributed/algorithms/join.py).  Ranks that run out of
+    # batches shadow every collective of a training iteration — the forward's
+    # buffer broadcast (from the highest still-training rank), the grad-sync flag,
+    # one all-reduce of zeros per bucket in bucket order (the same count, dtype
+    # and communicator as the bucketer's), the find-unused map — until all have
+    # joined; then the last joiner's parameters and buffers are broadcast.
+    def join(self, divide_by_initial_world_size: bool = True, enable: bool = True,
+             throw_on_early_termination: bool = False):
+        if not divide_by_initial_world_size:
+            raise NotImplementedError("join(divide_by_initial_world_size=False): the buckets are pre-scaled "
+                                      "by 1/world_size in the pack kernel")
+        if self._overlap is not None:
+            raise NotImplementedError("join() with the overlapped optimizer")
+        return Join([self], enable, throw_on_early_termination,
+                    divide_by_initial_world_size=divide_by_initial_world_size)
+
+    def join_hook(self, **kwargs) -> JoinHook:
+        return _DDPJoinHook(self)
+
+    @property
+    def join_device(self) -> torch.device:
+        return self.device
+
+    @property
+    def join_process_group(self):
+        return self.process_group
+
+    def _find_common_rank(self, input_rank: int, rank_cond: bool) -> int:
+        r = self._ctl_all_reduce(torch.tensor([input_rank if rank_cond else -1], dtype=torch.int64), "max")
+        v = int(r.item())
+        if v < 0:
+            raise ValueError("join: no rank qualified as the common rank")
+        return v
+
+    def _check_global_requires_backward_grad_sync(self, is_joined_rank: bool):
+        t = torch.tensor([1.0 if (not is_joined_rank and self.require_backward_grad_sync) else 0.0])
+        t = self._ctl_all_reduce(t, "sum")
+        return bool(t.item() != 0) if is_joined_rank else None
+
+    def _match_all_reduce_for_bwd_pass(self):
+        """A joined rank's side of one backward: an all-reduce of zeros per bucket,
+        in bucket order, through the path the training ranks' buckets take."""
+        b = self._bucketer
+        nb = len(b.buckets)
+        for bi, buf in enumerate(b.buffers):
+            z = torch.zeros_like(buf)
+            if self._comm_hook is not None:
+                state, hook = self._comm_hook
+                hook(state, GradBucket(bi, z, [self._params[i] for i in b.buckets[bi]], b.offsets_in_bucket[bi],
+                                       bi == nb - 1)).wait()
+            elif self._comm is not None:
+                self._comm.all_reduce(z, stream=L.stream_ptr(self.device))
+            elif z.is_cuda and self._backend == "gloo":
+                dist.all_reduce(z.cpu(), group=self.process_group)  # as _launch_external stages it
+            else:
+                dist.all_reduce(z, group=self.process_group)
+
+    def _sync_final_model(self, is_last_joiner: bool):
+        """After every rank joined: the last joiner's parameters (and buffers)
+        to all ranks (torch: _sync_module_states from the authoritative rank)."""
+        root = self._find_common_rank(self.rank, is_last_joiner)
+        seen, ts = set(), []
+        for n, p in self.module.named_parameters():
+            if n not in self.parameters_to_ignore and id(p) not in seen:
+                seen.add(id(p))
+                ts.append(p.detach())
+        if self.broadcast_buffers:
+            ts += self._module_buffers()
+        with torch.no_grad():
+            self._broadcast_tensors(ts, root)
+
     @staticmethod
     def _set_params_and_buffers_to_ignore_for_model(module, params_and_buffers_to_ignore):
         """torch's static helper (T:nn/parallel/distributed.py): names (as in
@@ -1228,6 +1310,30 @@ class DistributedDataParallel(nn.Module):
         nat = getattr(self, "_native", None)
         if nat is not None:
             nat.detach()
+
+
+class _DDPJoinHook(JoinHook):
+    """A joined rank's shadow of one DDP iteration (torch's _DDPJoinHook)."""
+
+    def __init__(self, ddp):
+        self.ddp = ddp
+        super().__init__()
+
+    def main_hook(self):
+        d = self.ddp
+        d._maybe_rebuild_buckets()
+        if d._will_sync_module_buffers():
+            d._sync_buffers(d._find_common_rank(d.rank, False))
+        should_sync = d._check_global_requires_backward_grad_sync(is_joined_rank=True)
+        d.require_forward_param_sync = should_sync
+        if not should_sync:
+            return
+        d._match_all_reduce_for_bwd_pass()
+        if d.find_unused_parameters:
+            d._ctl_all_reduce(torch.zeros(len(d._params), dtype=torch.int32), "max")  # the used map
+
+    def post_hook(self, is_last_joiner: bool):
+        self.ddp._sync_final_model(is_last_joiner)
 
 
 DDP = DistributedDataParallel

@@ -230,6 +230,61 @@ def test_params_and_buffers_to_ignore_match_torch():
     _run(_ignored, 2)
 
 
+def _uneven(rank, ws, opt_name):
+    """ddp.join() with uneven inputs (rank r has 2 + 2r batches): the same
+    weights, BN buffers and per-iteration grads as torch's DDP under its own
+    join, on every rank (the last joiner's model broadcast at the end)."""
+    import distributed_training_amd as D
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+
+    torch.manual_seed(0)
+    m1, m2 = _micro(), _micro()
+    m2.load_state_dict(m1.state_dict())
+    kw = dict(bucket_cap_mb=0.01)  # several buckets: the joined ranks shadow each in order
+    a = D.DistributedDataParallel(m1, **kw)
+    b = TDDP(m2, **kw)
+    mk = {"sgd": lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9),
+          "adam": lambda ps: torch.optim.Adam(ps, lr=1e-3),
+          # ws=3 is compared within a tolerance: a small plain step keeps the
+          # rounding differences from being amplified over six iterations
+          "sgd_small": lambda ps: torch.optim.SGD(ps, lr=1e-3)}[opt_name]
+    oa, ob = mk(a.parameters()), mk(b.parameters())
+    g = torch.Generator().manual_seed(40 + rank)
+    batches = [(torch.rand(3, 3, 32, 32, generator=g), torch.randint(0, 10, (3,), generator=g))
+               for _ in range(2 + 2 * rank)]
+    grads = {}
+    for tag, model, opt in (("a", a, oa), ("b", b, ob)):
+        with model.join():
+            for it, (x, y) in enumerate(batches):
+                opt.zero_grad()
+                nn.functional.cross_entropy(model(x), y).backward()
+                grads[(tag, it)] = [p.grad.clone() for p in model.module.parameters()]
+                opt.step()
+    # ws > 2: x(1/ws) before the sum (not exact for 3) and gloo's ring order
+    same = torch.equal if ws <= 2 else (lambda u, v: torch.allclose(u.double(), v.double(), rtol=1e-5, atol=1e-6))
+    for it in range(len(batches)):
+        for i, (u, v) in enumerate(zip(grads[("a", it)], grads[("b", it)])):
+            assert same(u, v), f"it {it} grad {i}"
+    for (n, x), y in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert same(x, y), n
+    # the final broadcast: every rank ends with the last joiner's model, bit for bit
+    for t in m1.state_dict().values():
+        lo, hi = t.double().clone(), t.double().clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        assert torch.equal(lo, hi)
+    assert a._has_rebuilt_buckets
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_join_uneven_inputs_match_torch(opt_name):
+    _run(_uneven, 2, opt_name)
+
+
+def test_join_uneven_inputs_ws3():
+    _run(_uneven, 3, "sgd_small")
+
+
 def _state_dict_keys(rank, ws):
     import distributed_training_amd as D
 

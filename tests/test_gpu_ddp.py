@@ -455,3 +455,72 @@ def test_mixed_dtype_buckets_ws1_rccl(cuda_device, rccl_pg):
         assert all(b.is_cuda for b in mddp._bucketer.buffers)
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+
+
+def _join_worker(rank, ws, port, errq):
+    """ddp.join() on the GPU (two ranks sharing cuda:0 over gloo, device buckets
+    staged through the host): rank 0 has 2 batches, rank 1 has 4.  While both
+    train, the averaged grads equal the oracle's Σ_r g_r·float(1/2); after rank 0
+    joined, rank 1's grads are its local grads ·float(1/2) (the joined rank's
+    zeros, divide_by_initial_world_size); afterwards both hold the last joiner's
+    weights."""
+    try:
+        import distributed_training_amd as D
+        from distributed_training_amd.resnet import micro_resnet
+
+        init_pg("gloo", rank, ws, port)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        torch.manual_seed(10 + rank)
+        model = micro_resnet().to(dev)
+        params = list(model.parameters())
+        local = {}
+        _snap_hooks(params, local)
+        ddp = D.DistributedDataParallel(model, collective="process_group", bucket_cap_mb=0.05)
+        opt = D.FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9)
+        g = torch.Generator(device=dev).manual_seed(100 + rank)
+        n = 2 + 2 * rank
+        with ddp.join():
+            for it in range(n):
+                x = torch.rand(6, 3, 32, 32, device=dev, generator=g)
+                y = torch.randint(0, 10, (6,), device=dev, generator=g)
+                torch.nn.functional.cross_entropy(ddp(x), y).backward()
+                torch.cuda.synchronize()
+                mine = [to_np(local[i]) for i in range(len(params))]
+                if it < 2:  # both ranks still training
+                    allg = [None] * ws
+                    dist.all_gather_object(allg, mine)
+                    avg = O.ddp_average(allg)
+                else:
+                    avg = O.ddp_average([[np.zeros_like(m) for m in mine], mine])
+                for i, p in enumerate(params):
+                    assert np.array_equal(to_np(p.grad), avg[i]), f"rank {rank} iter {it} param {i}"
+                opt.step()
+                opt.zero_grad()
+        w = [to_np(p) for p in params]
+        allw = [None] * ws
+        dist.all_gather_object(allw, w)
+        for a, b in zip(allw[0], allw[1]):
+            assert np.array_equal(a, b), "weights differ across ranks after join"
+        dist.destroy_process_group()
+    except BaseException as e:  # report to the parent
+        import traceback
+
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
+def test_ddp_join_uneven_inputs_ws2_one_gpu(cuda_device):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = free_port()
+    procs = [ctx.Process(target=_join_worker, args=(r, 2, port, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
