@@ -2,7 +2,8 @@
 launches — the unit a rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE) measures.
     python scripts/kernel_only.py <model> <launches> <op> [replicas]
 op: sgd | adam (update plan, as FusedSGD / FusedAdam build it),
-    pack | pack16 | unpack | unpacksq | sqnorm (bucket-layout plan, align 64)."""
+    pack | pack16 | unpack | unpacksq | sqnorm | sqpart (bucket-layout plan, align 64;
+    sqpart = gs_sqnorm_partial, the folded clip's Σg² launch)."""
 import os
 import sys
 
@@ -45,5 +46,7 @@ for _ in range(iters):
         plan.unpack(flat, 1, torch.float32, sqnorm=sq)
     elif op == "sqnorm":
         plan.sqnorm(1, torch.float32, sq)
+    elif op == "sqpart":
+        plan.sqnorm_partial(1, torch.float32)
 torch.cuda.synchronize()
 print("params", sum(n), "launches", iters, "op", op)
