@@ -81,6 +81,10 @@ def parse():
                          "curve at N>1 (distributed_training_amd.ddp.xgmi_bucket_caps)")
     ap.add_argument("--last-bucket-cap-mb", type=float, default=None,
                     help="cap the last bucket in gradient-ready order (the exposed end-of-backward chain)")
+    ap.add_argument("--leg-budget-s", type=float, default=300.0,
+                    help="N > 1: if the optional legs after the timed region (standalone collectives, parity, "
+                         "policy A/B) overrun this, print the line with the legs done so far and end every rank "
+                         "(0 = no watchdog)")
     ap.add_argument("--parity", type=int, default=1,
                     help="after the timed region: one self-checked step (distributed_training_amd.parity)")
     ap.add_argument("--kernel-rates", type=int, default=1,
@@ -649,64 +653,7 @@ def main():
             from distributed_training_amd import _lib as L
 
             zero_ms_saved = zero.plan.timer_read(kind=L.GS_OP_SGD if args.optimizer == "sgd" else L.GS_OP_ADAM)
-    tail = timeline = tail_timed = None
-    if zero is None and args.impl == "libgsync" and not args.graph:
-        # timed steps ran at timeline level 1: two events per step, the tail total
-        # (last bucket ready -> every bucket chain done) of the last timed step
-        tail_timed = ddp.tail_ms()
-        # the split (queue / pack / collective / unpack per bucket) needs ~4 events a
-        # bucket, ~10 µs each on the exposed tail: read it from untimed steps at level 2
-        ddp.set_timeline(2)
-        for _ in range(2):
-            step()
-        torch.cuda.synchronize()
-        comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # per bucket, HIP events on the comm stream
-        tail = ddp.tail_ms()
-        timeline = ddp.bucket_timeline_ms()
-        ddp.set_timeline(1)
-        opt.kernel_ms()  # drop the untimed steps' launches
-
-    coll = None
-    if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
-        coll = collective_bench(ddp, zero, world)
-    kernel_rates = None
-    if args.impl == "libgsync" and args.kernel_rates and rank == 0:
-        kernel_rates = grad_sync_kernel_rates([p for p in model.parameters() if p.requires_grad]
-                                              if zero is None else zero.params, dev)
-
-    parity = None
-    if args.parity and args.impl == "libgsync" and not args.graph:
-        from distributed_training_amd import parity as PC
-
-        if zero is None and args.engine == "colossal":
-            def fwd_bwd():
-                booster.backward(ccrit(cmodel(x), y), opt_w)
-
-            parity = PC.ddp_parity_step(ddp, opt_w, fwd_bwd)
-        elif zero is None:
-            def fwd_bwd():
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    loss = crit(ddp(x), y)
-                loss.backward()
-
-            parity = PC.ddp_parity_step(ddp, opt, fwd_bwd)
-        else:
-            def fwd_bwd():
-                crit(ddp(x).float(), y).backward()
-
-            parity = PC.zero_parity_step(zero, fwd_bwd)
-        if rank == 0:
-            print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
-
-    policy_ab = None
-    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
-    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
-            and not args.optimizer_overlap):
-        # after every reading of the headline DDP above: it is closed here
-        policy_ab = bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args)
-        if rank == 0:
-            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
-
+    # the headline's own numbers, complete before any leg below
     if args.impl == "torch":
         opt_ms = []
     elif zero is None and args.graph:
@@ -735,10 +682,6 @@ def main():
     opt_ms_avg = sum(opt_ms) / len(opt_ms) if opt_ms else None
     img_s = world * args.batch * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-
-    if rank != 0:
-        dist.destroy_process_group()
-        return
 
     upd_params = n_params if zero is None else n_params // world  # ZeRO updates this rank's shard
     achieved = bytes_per_param * upd_params / (opt_ms_avg * 1e-3) / 1e9 if opt_ms_avg else None
@@ -780,119 +723,230 @@ def main():
     else:
         log = {"has_rebuilt_buckets": 0}
         bucket_bytes = [b.numel() * b.element_size() for b in zero.grad_bufs]
-    grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
-    if comm_ms:
-        grad_sync["in_step_collective_ms"] = comm_ms
-    if world > 1 and comm_ms and min(comm_ms) > 0:
-        tot_ms = sum(comm_ms)
-        bus = sum(bucket_bytes) / (tot_ms * 1e-3) * 2 * (world - 1) / world / 1e9
-        peak = (world - 1) * XGMI_LINK_GBPS
-        grad_sync.update({"allreduce_ms_per_step": tot_ms, "allreduce_bus_GBps": bus, "xgmi_peak_GBps": peak,
-                          "frac": bus / peak, "per_bucket_ms": comm_ms,
-                          "note": "in-step: HIP events around each bucket collective on the comm stream, "
-                                  "an untimed step after the timed region (timeline level 2), includes "
-                                  "cross-rank arrival skew under backward"})
-    if coll is not None:
-        grad_sync["standalone"] = coll
-    if tail is not None:
-        # total: the last TIMED step (2 events a step); the split: an untimed step with
-        # every bucket's events (they stretch that step's tail by ~10 µs each)
-        grad_sync["tail_ms"] = dict(tail, total_timed_step=tail_timed["total"] if tail_timed else None,
-                                    split_from="untimed step at timeline level 2")
-        grad_sync["bucket_timeline_ms"] = timeline
-    if zero is None and args.impl == "libgsync":
-        grad_sync["bucket_policy"] = log.get("bucket_policy")
-        if log.get("xgmi_calibration"):
-            grad_sync["xgmi_calibration"] = log["xgmi_calibration"]
-    model_label = {"resnet18": "ResNet-18", "resnet50": "ResNet-50", "resnet152": "ResNet-152"}[args.model]
-    line = {
-        "metric": f"images/sec (node) {model_label} at 1/2/4/8 MI355X; grad-sync bus GB/s",
-        "value": img_s,
-        "unit": "images/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "fp16" if args.engine == "colossal" else "bf16",
-        "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
-        "config": {
-            "workload": (f"{args.model} synthetic 224x224 bf16 training, {args.batch} img/GPU, REFERENCE PATH for "
-                         f"the ZeRO-2 config: torch FSDP(SHARD_GRAD_OP, bf16 MixedPrecision) + clip 1.0 + "
-                         f"torch.optim.AdamW(fused=True) for comparison") if torch_zero else
-                        (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, "
-                         f"REFERENCE PATH for the Colossal config: torch DDP + torch.amp.GradScaler + "
-                         f"torch.optim.AdamW(fused=True) for comparison") if args.impl == "torch" and
-                        args.engine == "colossal" else
-                        (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
-                         f"REFERENCE PATH torch DDP + torch.optim.{'SGD' if args.optimizer == 'sgd' else 'Adam'}"
-                         f"(foreach) for comparison") if args.impl == "torch" else
-                        (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, Colossal "
-                         f"Booster(TorchDDPPlugin, mixed_precision='fp16') + HybridAdam as R:resnet/colossal/run.sh: "
-                         f"libgsync DDP (fp32 buckets, GradScaler inf check fused into the unpack) + fused Adam") if
-                        args.engine == "colossal" else
-                        (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
-                         f"{'one hipGraph per step: ' if args.graph else ''}libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
-                         f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}") if zero is None else
-                        (f"{args.model} synthetic 224x224 bf16 model training, {args.batch} img/GPU, libgsync "
-                         f"{args.engine.upper()} (bf16 {'reduce-scatter' if args.engine == 'zero2' else 'all-reduce'}"
-                         f" under backward, fp32 master shard, clip 1.0, fused "
-                         f"{'SGD' if args.optimizer == 'sgd' else 'AdamW'}, bf16 all-gather)"),
-            "engine": args.engine,
-            "global_batch": args.batch * world,
-            "per_gpu_batch": args.batch,
-            "parallelism": f"dp{world}",
-            "bucket_cap_mb": 25 if args.bucket_cap_mb is None else args.bucket_cap_mb,
-            "bucket_dtype": args.bucket_dtype,
-            "channels_last": not args.no_channels_last,
-            "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
-            "impl": args.impl,
-            "hipgraph": bool(args.graph),
-            "optimizer_overlap": bool(args.optimizer_overlap),
-            **({"rehearsal": "gloo, ranks sharing GPUs: control flow only, not a measurement"}
-               if args.pg_backend == "gloo" else {}),
-            "params": n_params,
-        },
-        "roofline": None if args.impl == "torch" else {
-            "kernel": ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
-                       if args.engine == "colossal" else
-                       f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update "
-                       f"(chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
-                       if zero is None else
-                       f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> "
-                       f"+ bf16 param write)"),
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS if achieved else None,
-            "copy_ceiling": HBM_COPY_GBPS,
-            "frac_of_copy_ceiling": achieved / HBM_COPY_GBPS if achieved else None,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
-            "avg_launch_ms": opt_ms_avg,
-            "launches": len(opt_ms),
-            "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
-                       + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
-                       + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
-                          if args.optimizer_overlap else "")),
-            "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
-            **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
-            **({"rocprof": trace_check} if trace_check else {}),
-        },
-        "grad_sync": grad_sync,
-        "grad_sync_kernels": kernel_rates,
-        "parity": parity,
-        **({"bucket_policy_ab": policy_ab} if policy_ab is not None else {}),
-        **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
-        "warmup_s": warm_s,
-        "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,
-                   "reserved_GB": torch.cuda.memory_reserved(dev) / 2**30,
-                   "device_total_GB": torch.cuda.get_device_properties(dev).total_memory / 2**30},
-        "has_rebuilt_buckets": log.get("has_rebuilt_buckets", 0),
-    }
+
+    def make_line():
+        grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
+        if comm_ms:
+            grad_sync["in_step_collective_ms"] = comm_ms
+        if world > 1 and comm_ms and min(comm_ms) > 0:
+            tot_ms = sum(comm_ms)
+            bus = sum(bucket_bytes) / (tot_ms * 1e-3) * 2 * (world - 1) / world / 1e9
+            peak = (world - 1) * XGMI_LINK_GBPS
+            grad_sync.update({"allreduce_ms_per_step": tot_ms, "allreduce_bus_GBps": bus, "xgmi_peak_GBps": peak,
+                              "frac": bus / peak, "per_bucket_ms": comm_ms,
+                              "note": "in-step: HIP events around each bucket collective on the comm stream, "
+                                      "an untimed step after the timed region (timeline level 2), includes "
+                                      "cross-rank arrival skew under backward"})
+        if coll is not None:
+            grad_sync["standalone"] = coll
+        if tail is not None:
+            # total: the last TIMED step (2 events a step); the split: an untimed step with
+            # every bucket's events (they stretch that step's tail by ~10 µs each)
+            grad_sync["tail_ms"] = dict(tail, total_timed_step=tail_timed["total"] if tail_timed else None,
+                                        split_from="untimed step at timeline level 2")
+            grad_sync["bucket_timeline_ms"] = timeline
+        if zero is None and args.impl == "libgsync":
+            grad_sync["bucket_policy"] = log.get("bucket_policy")
+            if log.get("xgmi_calibration"):
+                grad_sync["xgmi_calibration"] = log["xgmi_calibration"]
+        model_label = {"resnet18": "ResNet-18", "resnet50": "ResNet-50", "resnet152": "ResNet-152"}[args.model]
+        line = {
+            "metric": f"images/sec (node) {model_label} at 1/2/4/8 MI355X; grad-sync bus GB/s",
+            "value": img_s,
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp16" if args.engine == "colossal" else "bf16",
+            "data": "synthetic (torch.rand 224x224 images resident in HBM, random-init weights)",
+            "config": {
+                "workload": (f"{args.model} synthetic 224x224 bf16 training, {args.batch} img/GPU, REFERENCE PATH for "
+                             f"the ZeRO-2 config: torch FSDP(SHARD_GRAD_OP, bf16 MixedPrecision) + clip 1.0 + "
+                             f"torch.optim.AdamW(fused=True) for comparison") if torch_zero else
+                            (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, "
+                             f"REFERENCE PATH for the Colossal config: torch DDP + torch.amp.GradScaler + "
+                             f"torch.optim.AdamW(fused=True) for comparison") if args.impl == "torch" and
+                            args.engine == "colossal" else
+                            (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+                             f"REFERENCE PATH torch DDP + torch.optim.{'SGD' if args.optimizer == 'sgd' else 'Adam'}"
+                             f"(foreach) for comparison") if args.impl == "torch" else
+                            (f"{args.model} synthetic 224x224 fp16-autocast training, {args.batch} img/GPU, Colossal "
+                             f"Booster(TorchDDPPlugin, mixed_precision='fp16') + HybridAdam as R:resnet/colossal/run.sh: "
+                             f"libgsync DDP (fp32 buckets, GradScaler inf check fused into the unpack) + fused Adam") if
+                            args.engine == "colossal" else
+                            (f"{args.model} synthetic 224x224 bf16-autocast training, {args.batch} img/GPU, "
+                             f"{'one hipGraph per step: ' if args.graph else ''}libgsync DDP (bucketed RCCL all-reduce overlapped with backward) + fused "
+                             f"{'SGD-momentum/WD' if args.optimizer == 'sgd' else 'Adam'}") if zero is None else
+                            (f"{args.model} synthetic 224x224 bf16 model training, {args.batch} img/GPU, libgsync "
+                             f"{args.engine.upper()} (bf16 {'reduce-scatter' if args.engine == 'zero2' else 'all-reduce'}"
+                             f" under backward, fp32 master shard, clip 1.0, fused "
+                             f"{'SGD' if args.optimizer == 'sgd' else 'AdamW'}, bf16 all-gather)"),
+                "engine": args.engine,
+                "global_batch": args.batch * world,
+                "per_gpu_batch": args.batch,
+                "parallelism": f"dp{world}",
+                "bucket_cap_mb": 25 if args.bucket_cap_mb is None else args.bucket_cap_mb,
+                "bucket_dtype": args.bucket_dtype,
+                "channels_last": not args.no_channels_last,
+                "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
+                "impl": args.impl,
+                "hipgraph": bool(args.graph),
+                "optimizer_overlap": bool(args.optimizer_overlap),
+                **({"rehearsal": "gloo, ranks sharing GPUs: control flow only, not a measurement"}
+                   if args.pg_backend == "gloo" else {}),
+                "params": n_params,
+            },
+            "roofline": None if args.impl == "torch" else {
+                "kernel": ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
+                           if args.engine == "colossal" else
+                           f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update "
+                           f"(chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
+                           if zero is None else
+                           f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> "
+                           f"+ bf16 param write)"),
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+                "copy_ceiling": HBM_COPY_GBPS,
+                "frac_of_copy_ceiling": achieved / HBM_COPY_GBPS if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
+                "avg_launch_ms": opt_ms_avg,
+                "launches": len(opt_ms),
+                "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
+                           + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
+                           + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
+                              if args.optimizer_overlap else "")),
+                "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
+                **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
+                **({"rocprof": trace_check} if trace_check else {}),
+            },
+            "grad_sync": grad_sync,
+            "grad_sync_kernels": kernel_rates,
+            "parity": parity,
+            **({"bucket_policy_ab": policy_ab} if policy_ab is not None else {}),
+            **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
+            "warmup_s": warm_s,
+            "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,
+                       "reserved_GB": torch.cuda.memory_reserved(dev) / 2**30,
+                       "device_total_GB": torch.cuda.get_device_properties(dev).total_memory / 2**30},
+            "has_rebuilt_buckets": log.get("has_rebuilt_buckets", 0),
+        }
+        if leg_errors:
+            line["leg_errors"] = dict(leg_errors)
+        return line
+
+    # ---- after the timed region.  The headline is complete here; what follows are
+    # optional legs (tail split, standalone collectives, kernel rates, the parity
+    # step, the bucket-policy A/B).  Each leg that raises is recorded in
+    # "leg_errors" instead of losing the line; at N > 1 a watchdog prints the line
+    # with the legs completed so far and ends every rank if the legs overrun
+    # --leg-budget-s (a collective that never completes would otherwise cost the
+    # headline too).
+    tail = timeline = tail_timed = None
+    coll = kernel_rates = parity = policy_ab = None
+    leg_errors: dict = {}
+    current_leg = ["start"]
+
+    def leg(name, fn):
+        current_leg[0] = name
+        try:
+            return fn()
+        except Exception as ex:  # recorded, the line still prints
+            import traceback
+
+            leg_errors[name] = repr(ex)
+            print(f"[bench] leg {name} failed: {ex!r}\n{traceback.format_exc()}", file=sys.stderr, flush=True)
+            return None
+
+    watchdog = None
+    if world > 1 and args.leg_budget_s > 0:
+        import threading
+
+        def expire():
+            if rank == 0:
+                ln = make_line()
+                ln["legs_incomplete"] = {"leg": current_leg[0], "budget_s": args.leg_budget_s}
+                print(json.dumps(ln), flush=True)
+            print(f"[bench] rank {rank}: legs overran {args.leg_budget_s}s in {current_leg[0]}: exiting",
+                  file=sys.stderr, flush=True)
+            os._exit(0)
+
+        watchdog = threading.Timer(args.leg_budget_s, expire)
+        watchdog.daemon = True
+        watchdog.start()
+
+    def tail_leg():
+        nonlocal tail, timeline, tail_timed, comm_ms
+        if zero is None and args.impl == "libgsync" and not args.graph:
+            # timed steps ran at timeline level 1: two events per step, the tail total
+            # (last bucket ready -> every bucket chain done) of the last timed step
+            tail_timed = ddp.tail_ms()
+            # the split (queue / pack / collective / unpack per bucket) needs ~4 events a
+            # bucket, ~10 µs each on the exposed tail: read it from untimed steps at level 2
+            ddp.set_timeline(2)
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            comm_ms = [m for m in ddp.bucket_comm_ms() if m >= 0]  # per bucket, HIP events on the comm stream
+            tail = ddp.tail_ms()
+            timeline = ddp.bucket_timeline_ms()
+            ddp.set_timeline(1)
+            opt.kernel_ms()  # drop the untimed steps' launches
+
+
+    leg("tail_split", tail_leg)
+    if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
+        coll = leg("collective_bench", lambda: collective_bench(ddp, zero, world))
+    if args.impl == "libgsync" and args.kernel_rates and rank == 0:
+        kernel_rates = leg("kernel_rates", lambda: grad_sync_kernel_rates(
+            [p for p in model.parameters() if p.requires_grad] if zero is None else zero.params, dev))
+
+    if args.parity and args.impl == "libgsync" and not args.graph:
+        from distributed_training_amd import parity as PC
+
+        if zero is None and args.engine == "colossal":
+            def fwd_bwd():
+                booster.backward(ccrit(cmodel(x), y), opt_w)
+
+            parity = leg("parity", lambda: PC.ddp_parity_step(ddp, opt_w, fwd_bwd))
+        elif zero is None:
+            def fwd_bwd():
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = crit(ddp(x), y)
+                loss.backward()
+
+            parity = leg("parity", lambda: PC.ddp_parity_step(ddp, opt, fwd_bwd))
+        else:
+            def fwd_bwd():
+                crit(ddp(x).float(), y).backward()
+
+            parity = leg("parity", lambda: PC.zero_parity_step(zero, fwd_bwd))
+        if rank == 0:
+            print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
+
+    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
+    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
+            and not args.optimizer_overlap):
+        # after every reading of the headline DDP above: it is closed here
+        policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
+        if rank == 0 and policy_ab is not None:
+            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
+    current_leg[0] = "done"
+    if watchdog is not None:
+        watchdog.cancel()
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    line = make_line()
     if args.cpu_baseline and world == 1:
         from oracle.cpu_ddp_baseline import cpu_model_name, run as cpu_run
 

@@ -205,3 +205,20 @@ def test_bench_multirank_gloo_rehearsal(cuda_device, engine, n):
         assert d["roofline"]["algorithmic_bytes_per_launch"] == 20 * (d["config"]["params"] // n)
     else:
         assert par["buffers_identical"] is True
+
+
+def test_bench_leg_watchdog_keeps_the_headline(cuda_device):
+    """N>1: optional legs that overrun --leg-budget-s (here: 1 s, so the first
+    leg overruns) end every rank with exit 0 after rank 0 printed the line —
+    the headline and roofline intact, the unfinished leg named."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--leg-budget-s", "1", "--kernel-rates", "0",
+           "--policy-ab", "1"] + SMALL
+    p = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=500)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = lines[0]
+    assert d["legs_incomplete"]["budget_s"] == 1.0 and d["legs_incomplete"]["leg"] != "done"
+    assert d["value"] > 0 and d["roofline"]["achieved"] > 0 and d["n_gpus"] == 2
