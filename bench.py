@@ -81,6 +81,9 @@ def parse():
                          "curve at N>1 (distributed_training_amd.ddp.xgmi_bucket_caps)")
     ap.add_argument("--last-bucket-cap-mb", type=float, default=None,
                     help="cap the last bucket in gradient-ready order (the exposed end-of-backward chain)")
+    ap.add_argument("--zero-leg", type=int, default=-1,
+                    help="after the headline: BASELINE configs[3] (ZeRO-2, bf16 ResNet-50) timed on the same "
+                         "ranks, reported as the line's `zero2` object (-1: at N > 1 on the DDP engine)")
     ap.add_argument("--leg-budget-s", type=float, default=300.0,
                     help="N > 1: if the optional legs after the timed region (standalone collectives, parity, "
                          "policy A/B) overrun this, print the line with the legs done so far and end every rank "
@@ -377,6 +380,67 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
             "rule": f"a variant becomes the default if images/s >= (1 + {POLICY_MARGIN}) x the mean of the two "
                     "torch-layout runs with parity.ok (DESIGN §8); best such variant wins",
             "decision": best}
+
+
+def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
+    """BASELINE configs[3] inside the N > 1 run: a fresh ResNet-50 in bf16 on the
+    libgsync ZeRO-2 engine as the DeepSpeed config drives it
+    (R:resnet/deepspeed/deepspeed_train.py:170-219: bf16, stage 2, AdamW,
+    gradient_clipping 1.0, reduce_bucket_size 5e7; reduce-scatter of bf16
+    grads, fp32 master shard update, all-gather of bf16 params) on the same
+    communicator, `steps` timed steps (MAX over ranks) and one self-checked
+    step.  The headline line is the DDP engine; this object is configs[3] at
+    the same N."""
+    import distributed_training_amd as D  # noqa: F401
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd import parity as PC
+    from distributed_training_amd.resnet import MODELS
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    torch.manual_seed(0)
+    model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
+    zero = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=1e-3, momentum=0.9, weight_decay=3e-7,
+                            reduce_bucket_size=int(5e7), gradient_clipping=1.0)
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
+    x = x.to(torch.bfloat16)
+    y = torch.randint(0, 1000, (args.batch,), device=dev, generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def fwd_bwd():
+        crit(model(x).float(), y).backward()
+
+    def one():
+        zero.prepare_backward()
+        fwd_bwd()
+        zero.step()
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    zero.plan.timer_enable(4 * steps + 8)
+    coll_h.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    coll_h.barrier()
+    el = coll_h.max(time.perf_counter() - t0)
+    upd = zero.plan.timer_read(kind=L.GS_OP_ADAM)
+    zero.plan.timer_enable(0)
+    shard = sum(p.numel() for p in zero.params) // world
+    upd_ms = sum(upd) / len(upd) if upd else None
+    out = {"engine": "zero2", "config": "BASELINE configs[3]: ResNet-50 bf16 model, ZeRO-2 reduce-scatter + "
+                                        "AdamW on fp32 master shards + all-gather, clip 1.0",
+           "images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3,
+           "per_gpu_batch": args.batch, "steps": steps, "warmup": warmup,
+           "shard_update": {"avg_launch_ms": upd_ms, "alg_bytes_per_launch": 28 * shard,
+                            "frac": 28 * shard / (upd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if upd_ms else None}}
+    out["parity"] = PC.zero_parity_step(zero, fwd_bwd)
+    zero.close()
+    del zero, model
+    torch.cuda.empty_cache()
+    return out
 
 
 class _OverlappedStep:
@@ -831,6 +895,7 @@ def main():
             "grad_sync_kernels": kernel_rates,
             "parity": parity,
             **({"bucket_policy_ab": policy_ab} if policy_ab is not None else {}),
+        **({"zero2": zero2} if zero2 is not None else {}),
             **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
             "warmup_s": warm_s,
             "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,
@@ -850,7 +915,7 @@ def main():
     # --leg-budget-s (a collective that never completes would otherwise cost the
     # headline too).
     tail = timeline = tail_timed = None
-    coll = kernel_rates = parity = policy_ab = None
+    coll = kernel_rates = parity = policy_ab = zero2 = None
     leg_errors: dict = {}
     current_leg = ["start"]
 
@@ -938,6 +1003,12 @@ def main():
         policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
         if rank == 0 and policy_ab is not None:
             print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
+    want_zero = args.zero_leg == 1 or (args.zero_leg == -1 and world > 1)
+    if want_zero and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
+        zero2 = leg("zero2", lambda: zero2_leg(args, world, rank, dev, coll_h))
+        if rank == 0 and zero2 is not None:
+            print(f"[bench] zero2 leg: {zero2['images_per_sec']:.1f} images/s, parity {zero2['parity'].get('ok')}",
+                  file=sys.stderr, flush=True)
     current_leg[0] = "done"
     if watchdog is not None:
         watchdog.cancel()

@@ -109,6 +109,11 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     assert "rehearsal" in lines[0]["config"]
     assert lines[0]["parity"]["collective"] == "gloo"
     _check_policy_ab(lines[0], 2)
+    # BASELINE configs[3] timed in the same N>1 run: the ZeRO-2 leg
+    z = lines[0]["zero2"]
+    assert z["engine"] == "zero2" and z["images_per_sec"] > 0 and z["shard_update"]["avg_launch_ms"] > 0
+    assert z["parity"]["ok"] is True and z["parity"]["world"] == 2, z["parity"]
+    assert "leg_errors" not in lines[0], lines[0].get("leg_errors")
 
 
 def _check_policy_ab(d, n):
