@@ -84,7 +84,11 @@ def parse():
     ap.add_argument("--zero-leg", type=int, default=-1,
                     help="after the headline: BASELINE configs[3] (ZeRO-2, bf16 ResNet-50) timed on the same "
                          "ranks, reported as the line's `zero2` object (-1: at N > 1 on the DDP engine)")
-    ap.add_argument("--leg-budget-s", type=float, default=300.0,
+    ap.add_argument("--colossal-leg", type=int, default=-1,
+                    help="after the headline: BASELINE configs[4] (Colossal shim, ResNet-152 fp32 grads, fp16 "
+                         "autocast, HybridAdam, 128 img/GPU) on the same ranks, the line's `colossal` object "
+                         "(-1: at N > 1 on the DDP engine)")
+    ap.add_argument("--leg-budget-s", type=float, default=420.0,
                     help="N > 1: if the optional legs after the timed region (standalone collectives, parity, "
                          "policy A/B) overrun this, print the line with the legs done so far and end every rank "
                          "(0 = no watchdog)")
@@ -439,6 +443,60 @@ def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
     out["parity"] = PC.zero_parity_step(zero, fwd_bwd)
     zero.close()
     del zero, model
+    torch.cuda.empty_cache()
+    return out
+
+
+def colossal_leg(args, world, rank, dev, coll_h, batch=128, steps=8, warmup=3):
+    """BASELINE configs[4] inside the N > 1 run: a fresh ResNet-152 (fp32
+    params and grads, 240.8 MB all-reduced a step) through the Colossal shim as
+    R:resnet/colossal/run.sh drives it (TorchDDPPlugin, mixed_precision='fp16',
+    HybridAdam(lr=1e-3*ws), R:resnet/colossal/colossal_train.py:118-161):
+    libgsync DDP underneath, GradScaler's inf check fused into the unpack.
+    `steps` timed steps (MAX over ranks) and one self-checked step."""
+    import distributed_training_amd as D
+    from distributed_training_amd import parity as PC
+    from distributed_training_amd.compat import colossalai as C
+    from distributed_training_amd.resnet import MODELS
+
+    torch.manual_seed(0)
+    name = "resnet152" if args.model == "resnet50" else args.model  # small rehearsals keep their small model
+    model = MODELS[name](num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
+    opt = C.HybridAdam(model.parameters(), lr=1e-3 * world)
+    cmodel, opt_w, ccrit, _, _ = booster.boost(model, opt, criterion=torch.nn.CrossEntropyLoss())
+    ddp = next(m for m in cmodel.modules() if isinstance(m, D.DistributedDataParallel))
+    g = torch.Generator(device=dev).manual_seed(5678 + rank)
+    x = torch.rand(batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (batch,), device=dev, generator=g)
+
+    def fwd_bwd():
+        booster.backward(ccrit(cmodel(x), y), opt_w)
+
+    def one():
+        fwd_bwd()
+        opt_w.step()
+        opt_w.zero_grad()
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    coll_h.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    coll_h.barrier()
+    el = coll_h.max(time.perf_counter() - t0)
+    out = {"engine": "colossal", "model": name,
+           "config": "BASELINE configs[4]: ResNet-152 fp32 params/grads through the Colossal "
+                     "Booster(TorchDDPPlugin, fp16) + HybridAdam, libgsync DDP underneath",
+           "images_per_sec": world * batch * steps / el, "ms_per_step": el / steps * 1e3, "per_gpu_batch": batch,
+           "steps": steps, "warmup": warmup, "grad_bytes_per_step": 4 * sum(p.numel() for p in ddp._params)}
+    out["parity"] = PC.ddp_parity_step(ddp, opt_w, fwd_bwd)
+    opt_w.zero_grad()
+    ddp.close()
+    del cmodel, opt_w, ddp, model
     torch.cuda.empty_cache()
     return out
 
@@ -896,6 +954,7 @@ def main():
             "parity": parity,
             **({"bucket_policy_ab": policy_ab} if policy_ab is not None else {}),
         **({"zero2": zero2} if zero2 is not None else {}),
+        **({"colossal": colossal} if colossal is not None else {}),
             **({} if zero is None else {"zero_step_window_ms": sum(win_ms) / len(win_ms)}),
             "warmup_s": warm_s,
             "memory": {"max_allocated_GB": torch.cuda.max_memory_allocated(dev) / 2**30,
@@ -915,7 +974,7 @@ def main():
     # --leg-budget-s (a collective that never completes would otherwise cost the
     # headline too).
     tail = timeline = tail_timed = None
-    coll = kernel_rates = parity = policy_ab = zero2 = None
+    coll = kernel_rates = parity = policy_ab = zero2 = colossal = None
     leg_errors: dict = {}
     current_leg = ["start"]
 
@@ -1009,6 +1068,13 @@ def main():
         if rank == 0 and zero2 is not None:
             print(f"[bench] zero2 leg: {zero2['images_per_sec']:.1f} images/s, parity {zero2['parity'].get('ok')}",
                   file=sys.stderr, flush=True)
+    want_col = args.colossal_leg == 1 or (args.colossal_leg == -1 and world > 1)
+    if want_col and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
+        colossal = leg("colossal", lambda: colossal_leg(args, world, rank, dev, coll_h,
+                                                        batch=min(128, args.batch)))
+        if rank == 0 and colossal is not None:
+            print(f"[bench] colossal leg: {colossal['images_per_sec']:.1f} images/s, "
+                  f"parity {colossal['parity'].get('ok')}", file=sys.stderr, flush=True)
     current_leg[0] = "done"
     if watchdog is not None:
         watchdog.cancel()

@@ -113,6 +113,8 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     z = lines[0]["zero2"]
     assert z["engine"] == "zero2" and z["images_per_sec"] > 0 and z["shard_update"]["avg_launch_ms"] > 0
     assert z["parity"]["ok"] is True and z["parity"]["world"] == 2, z["parity"]
+    c = lines[0]["colossal"]  # BASELINE configs[4] in the same run
+    assert c["engine"] == "colossal" and c["images_per_sec"] > 0 and c["parity"]["ok"] is True, c["parity"]
     assert "leg_errors" not in lines[0], lines[0].get("leg_errors")
 
 
