@@ -190,8 +190,6 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     flat16 = torch.zeros(plan.flat_numel, device=dev, dtype=torch.bfloat16)
     sq = torch.zeros(1, device=dev)
 
-    batched = [None]
-
     def rate(fn, p_):
         for _ in range(3):
             fn()
@@ -200,16 +198,6 @@ def grad_sync_kernel_rates(params, dev, iters=20):
             fn()
         ts = p_.timer_read()
         p_.timer_enable(0)
-        # and the same calls back to back between ONE event pair (launch gaps
-        # included, no per-launch event cost): what a stream of them sustains
-        st = torch.cuda.current_stream(dev)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(st)
-        for _ in range(iters):
-            fn()
-        b.record(st)
-        torch.cuda.synchronize(dev)
-        batched[0] = a.elapsed_time(b) / iters
         return sum(ts) / iters  # per call: every launch the call makes counts
 
     rows = {}
@@ -220,7 +208,7 @@ def grad_sync_kernel_rates(params, dev, iters=20):
             ("unpack_f32+sqnorm", 8 * n, lambda: plan.unpack(flat, 1, torch.float32, sqnorm=sq)),
             ("sqnorm_f32", 4 * n, lambda: plan.sqnorm(1, torch.float32, sq))):
         ms = rate(fn, plan)
-        rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9, "batched_ms": batched[0]}
+        rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9}
     up = TensorListPlan(numels, dev, task_units=update_task_units(dev))
     ps = [torch.randn(p.shape, device=dev, generator=g) for p in params]
     bs = [torch.randn(p.shape, device=dev, generator=g) * 0.01 for p in params]
@@ -229,14 +217,12 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     up.set_ptrs(1, grads)
     up.set_ptrs(2, bs)
     ms = rate(lambda: up.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False), up)
-    rows["sgd_momentum_wd"] = {"alg_bytes": 20 * n, "avg_ms": ms, "GBps": 20 * n / (ms * 1e-3) / 1e9,
-                               "batched_ms": batched[0]}
+    rows["sgd_momentum_wd"] = {"alg_bytes": 20 * n, "avg_ms": ms, "GBps": 20 * n / (ms * 1e-3) / 1e9}
     # the clip path as the folded clip runs it (DeepSpeed gradient_clipping,
     # R:resnet/deepspeed/deepspeed_train.py:195): Σg² partial sums, then the update
     # whose workgroups form the coefficient from them — both launches timed
     ms = rate(lambda: up.sqnorm_partial(1, torch.float32), up)
-    rows["sqnorm_partial_f32"] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9,
-                                  "batched_ms": batched[0]}
+    rows["sqnorm_partial_f32"] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9}
     clip_out = torch.zeros(3, device=dev)
 
     def clipped_sgd():
@@ -247,18 +233,16 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     ms = rate(clipped_sgd, up)
     up.set_clip(None)
     rows["clip_path_sgd"] = {"alg_bytes": 24 * n, "avg_ms": ms, "GBps": 24 * n / (ms * 1e-3) / 1e9,
-                             "batched_ms": batched[0], "launches": "sqnorm_partial + clipped sgd"}
+                             "launches": "sqnorm_partial + clipped sgd"}
     up.set_ptrs(3, vs)
     ms = rate(lambda: up.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5), up)
-    rows["adam"] = {"alg_bytes": 28 * n, "avg_ms": ms, "GBps": 28 * n / (ms * 1e-3) / 1e9, "batched_ms": batched[0]}
+    rows["adam"] = {"alg_bytes": 28 * n, "avg_ms": ms, "GBps": 28 * n / (ms * 1e-3) / 1e9}
     for r in rows.values():
         r["frac"] = r["GBps"] / HBM_PEAK_GBPS
-        if r.get("batched_ms"):
-            r["batched_frac"] = r["alg_bytes"] / (r["batched_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS
     return {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS,
-            "timing": "after the timed region, warm, alone on the GPU; frac: plan launch timer (HIP events on the "
-                      f"launch stream around each kernel), average of {iters} calls; batched_frac: the same {iters} "
-                      "calls back to back between one event pair",
+            "timing": "after the timed region, warm, alone on the GPU; plan launch timer (HIP events on the "
+                      f"launch stream around each kernel), average of {iters} calls (kernel-trace durations: "
+                      "profiles/r3/r3i_trace_rates.json)",
             "min_frac": min(r["frac"] for r in rows.values())}
 
 
