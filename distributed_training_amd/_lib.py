@@ -137,6 +137,7 @@ SIGNATURES = {
     "gs_bucketer_finalize": (_c_int, [_vp, _vp]),
     "gs_bucketer_unpack_bucket": (_c_int, [_vp, _c_int, _vp]),
     "gs_bucketer_set_found_inf": (_c_int, [_vp, _vp]),
+    "gs_bucketer_set_div_factor": (_c_int, [_vp, _c_f]),
     "gs_bucketer_set_debug": (_c_int, [_vp, _vp]),
     "gs_bucketer_set_bucket_dtype": (_c_int, [_vp, _c_int, _c_int, _c_int]),
     "gs_bucketer_last_comm_ms": (_c_int, [_vp, _c_int, _p_f]),

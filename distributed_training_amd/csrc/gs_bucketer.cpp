@@ -505,6 +505,14 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
   return GS_OK;
 }
 
+int gs_bucketer_set_div_factor(gs_bucketer* b, float div_factor) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_set_div_factor: NULL bucketer");
+  GS_CHECK_ARG(div_factor > 0.f, "gs_bucketer_set_div_factor: div_factor must be > 0");
+  std::lock_guard<std::mutex> lk(b->mu);
+  b->div = div_factor;
+  return GS_OK;
+}
+
 int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf) {
   GS_CHECK_ARG(b != nullptr, "gs_bucketer_set_found_inf: NULL bucketer");
   GS_CHECK_ARG(!(b->flags & (GS_BKT_REDUCE_SCATTER | GS_BKT_NO_UNPACK)) || found_inf == nullptr,

@@ -296,6 +296,7 @@ class DistributedDataParallel(nn.Module, Joinable):
                  collective: str = "auto", bucket_policy: str = "torch", last_bucket_cap_mb=None):
         super().__init__()
         Joinable.__init__(self)  # the join config (disabled until a Join context enables it)
+        self._divide_by_initial_world_size = True
         if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
             raise NotImplementedError("delay_all_reduce_named_params is outside the gradient-sync path")
         if mixed_precision is not None or device_mesh is not None:
@@ -441,6 +442,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         if old is not None:
             old.close()
         b = _Bucketer(self, buckets, self._flags())
+        self._div_factor = float(self.world_size)  # a new bucketer divides by the world size
         t = getattr(self, "_found_inf_target", None)
         if t is not None:
             L.check(L.lib().gs_bucketer_set_found_inf(b.handle, t.data_ptr()), "gs_bucketer_set_found_inf")
@@ -679,9 +681,16 @@ class DistributedDataParallel(nn.Module, Joinable):
         grad_sync = torch.is_grad_enabled() and self.require_backward_grad_sync
         # under ddp.join(): tell the joined ranks this one is still training (their
         # Join context counts these), as torch's forward does
-        Join.notify_join_context(self)
+        work = Join.notify_join_context(self)
         if grad_sync:
             self._maybe_rebuild_buckets()
+        if work is not None and not self._divide_by_initial_world_size:
+            # divide by the ranks still training (torch: the Reducer waits on this work
+            # for its div_factor_); a host read, in join mode only
+            work.wait()
+            self._set_div_factor(float(work.result()[0].item()))
+        elif self._div_factor != self.world_size and not self._join_config.enable:
+            self._set_div_factor(float(self.world_size))
         joining = self._join_config.enable
         if self._will_sync_module_buffers():
             # under join rank 0 may have stopped: the highest still-training rank is the source
@@ -1201,16 +1210,21 @@ class DistributedDataParallel(nn.Module, Joinable):
     # joined; then the last joiner's parameters and buffers are broadcast.
     def join(self, divide_by_initial_world_size: bool = True, enable: bool = True,
              throw_on_early_termination: bool = False):
-        if not divide_by_initial_world_size:
-            raise NotImplementedError("join(divide_by_initial_world_size=False): the buckets are pre-scaled "
-                                      "by 1/world_size in the pack kernel")
         if self._overlap is not None:
             raise NotImplementedError("join() with the overlapped optimizer")
         return Join([self], enable, throw_on_early_termination,
                     divide_by_initial_world_size=divide_by_initial_world_size)
 
     def join_hook(self, **kwargs) -> JoinHook:
+        self._divide_by_initial_world_size = kwargs.get("divide_by_initial_world_size", True)
         return _DDPJoinHook(self)
+
+    def _set_div_factor(self, div: float):
+        """The packs' divisor for the next backward (gs_bucketer_set_div_factor)."""
+        if div != self._div_factor:
+            L.check(L.lib().gs_bucketer_set_div_factor(self._bucketer.handle, float(div)),
+                    "gs_bucketer_set_div_factor")
+            self._div_factor = div
 
     @property
     def join_device(self) -> torch.device:

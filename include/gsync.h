@@ -341,6 +341,12 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream);
  * zeroes it before backward); NULL disables.  Replaces the check pass of
  * GradScaler._unscale_grads_ (T:amp/grad_scaler.py:280) for these grads. */
 int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf);
+/* The divisor of the next backward's packs (grad x float(1/div_factor)),
+ * between backwards: DDP.join(divide_by_initial_world_size=False) divides by
+ * the ranks still training, as the Reducer's div_factor_ set from the forward
+ * pass work handle (T:include/torch/csrc/distributed/c10d/reducer.hpp:499,
+ * _set_forward_pass_work_handle). */
+int gs_bucketer_set_div_factor(gs_bucketer* b, float div_factor);
 int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
 /* timing of the library's own collective launches (ms of the last iteration, via events) */
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);

@@ -230,7 +230,7 @@ def test_params_and_buffers_to_ignore_match_torch():
     _run(_ignored, 2)
 
 
-def _uneven(rank, ws, opt_name):
+def _uneven(rank, ws, opt_name, divide_initial=True):
     """ddp.join() with uneven inputs (rank r has 2 + 2r batches): the same
     weights, BN buffers and per-iteration grads as torch's DDP under its own
     join, on every rank (the last joiner's model broadcast at the end)."""
@@ -254,7 +254,7 @@ def _uneven(rank, ws, opt_name):
                for _ in range(2 + 2 * rank)]
     grads = {}
     for tag, model, opt in (("a", a, oa), ("b", b, ob)):
-        with model.join():
+        with model.join(divide_by_initial_world_size=divide_initial):
             for it, (x, y) in enumerate(batches):
                 opt.zero_grad()
                 nn.functional.cross_entropy(model(x), y).backward()
@@ -283,6 +283,13 @@ def test_join_uneven_inputs_match_torch(opt_name):
 
 def test_join_uneven_inputs_ws3():
     _run(_uneven, 3, "sgd_small")
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_join_divide_by_remaining_ranks(ws):
+    """divide_by_initial_world_size=False: the grads are averaged over the ranks
+    still training (the packs' divisor set per iteration from the join count)."""
+    _run(_uneven, ws, "sgd" if ws == 2 else "sgd_small", False)
 
 
 def _state_dict_keys(rank, ws):
