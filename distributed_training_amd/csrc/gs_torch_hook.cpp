@@ -68,8 +68,11 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
  public:
   // constructed from Python (GIL held): the callable is kept as a plain
   // reference, so the destructor never needs pybind11's GIL machinery
-  Hooks(std::vector<at::Tensor> params, int device, py::function on_finalize)
-      : params_(std::move(params)), device_(device), on_finalize_(on_finalize.release().ptr()) {
+  // release: the ZeRO engine's mode — a grad is released from its parameter
+  // once marked ready (DeepSpeed frees it too) and held until its bucket's
+  // pack is enqueued, then recorded on the comm stream for the allocator
+  Hooks(std::vector<at::Tensor> params, int device, py::function on_finalize, bool release)
+      : params_(std::move(params)), device_(device), on_finalize_(on_finalize.release().ptr()), release_(release) {
     dense_strides_.resize(params_.size());
     dense_seen_.assign(params_.size(), 0);
     accs_.resize(params_.size());
@@ -93,6 +96,7 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
 
   void detach() {
     active_ = false;
+    pinned_.clear();
     for (size_t i = 0; i < accs_.size(); ++i) {
       if (auto a = accs_[i].lock()) a->del_post_hook(keys_[i]);
       accs_[i].reset();
@@ -101,9 +105,16 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
 
   bool attached() const { return active_; }
 
-  void set_bucketer(uintptr_t handle, int n_buckets) {
+  // bucket_of: each parameter's bucket (release mode); comm_stream: where the
+  // library runs the packs (release mode: held grads are recorded on it)
+  void set_bucketer(uintptr_t handle, int n_buckets, std::vector<int> bucket_of, uintptr_t comm_stream) {
     b_ = reinterpret_cast<gs_bucketer*>(handle);
     ready_.assign(static_cast<size_t>(std::max(1, n_buckets)), 0);  // mark_ready's ready-bucket list
+    bucket_of_ = std::move(bucket_of);
+    held_.assign(static_cast<size_t>(std::max(1, n_buckets)), {});
+    comm_stream_ = reinterpret_cast<void*>(comm_stream);
+    if (release_ && b_ != nullptr && bucket_of_.size() != params_.size())
+      throw std::runtime_error("_gshook: release mode needs every parameter's bucket");
   }
 
   // forward of a synchronising step (ddp._prepare_for_backward): arms the hooks
@@ -115,12 +126,18 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     if (active_) arm();
   }
 
-  // one post-hook on each parameter's AccumulateGrad in the graph just built
-  // (a node that outlived its graph, e.g. retain_graph, keeps its one hook)
+  // one post-hook on each parameter's AccumulateGrad: the node of the graph just
+  // built (DDP arms after its forward), or — armed before the forward, as the
+  // ZeRO engine's prepare_backward is — a node created now, on the current
+  // stream, that the coming forward adopts (the variable holds its node weakly:
+  // it is pinned here until finalize).  A node that outlived its graph
+  // (retain_graph) keeps its one hook.
   void arm() {
+    pinned_.clear();
     for (size_t i = 0; i < params_.size(); ++i) {
-      auto a = torch::autograd::impl::try_get_grad_accumulator(params_[i]);
-      if (!a) continue;  // not in this graph
+      auto a = torch::autograd::impl::grad_accumulator(params_[i]);
+      if (!a) continue;
+      pinned_.push_back(a);
       if (accs_[i].lock() == a) continue;
       keys_[i] = a->add_post_hook(std::make_unique<MarkReady>(this, static_cast<int>(i)));
       accs_[i] = a;
@@ -140,6 +157,7 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     }
     if (record_order_) order_.push_back(i);
     const at::Tensor& p = params_[i];
+    if (release_) return on_grad_release(i, p);
     at::Tensor& g = p.mutable_grad();
     if (!g.defined()) throw std::runtime_error("_gshook: gradient hook fired without a gradient");
     // fast path: strides of a parameter already seen dense (grads in that layout are too)
@@ -158,10 +176,38 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     if (rc < 0) throw std::runtime_error(std::string("gs_bucketer_mark_ready: ") + gs_last_error());
   }
 
+  void on_grad_release(int i, const at::Tensor& p) {
+    at::Tensor g = p.grad();
+    if (!g.defined()) throw std::runtime_error("_gshook: gradient hook fired without a gradient");
+    if (!dense_like(g, p)) {
+      at::Tensor dense = at::empty_like(p);
+      dense.copy_(g);
+      g = dense;
+    }
+    const int bk = bucket_of_[i];
+    held_[bk].push_back(g);
+    p.mutable_grad() = at::Tensor();  // released: the bucket holds the data from here on
+    int32_t n_ready = 0;
+    const int rc = gs_bucketer_mark_ready(b_, i, g.data_ptr(), stream_, ready_.data(), &n_ready);
+    if (rc < 0) throw std::runtime_error(std::string("gs_bucketer_mark_ready: ") + gs_last_error());
+    for (int k = 0; k < n_ready; ++k) {
+      auto& hs = held_[ready_[k]];
+      if (comm_stream_ != nullptr) {
+        // the pack on the comm stream is enqueued: the allocator may reuse these
+        // grads' memory only after it has run
+        const c10::Stream cs = c10::hip::getStreamFromExternal(static_cast<hipStream_t>(comm_stream_),
+                                                                static_cast<c10::DeviceIndex>(device_));
+        for (auto& t : hs) t.record_stream(cs);
+      }
+      hs.clear();
+    }
+  }
+
   void finalize() {
     const int rc = gs_bucketer_finalize(b_, stream_);
     in_backward_ = false;
     finalize_queued_ = false;
+    pinned_.clear();
     if (rc < 0) throw std::runtime_error(std::string("gs_bucketer_finalize: ") + gs_last_error());
     // the Python DDP's bookkeeping (ddp._native_finalized), once per backward
     std::string err;
@@ -194,6 +240,7 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
   int device_;
   PyObject* on_finalize_;  // strong reference (see the constructor)
   std::vector<std::weak_ptr<Node>> accs_;  // the node each hook is on (owned by its graph)
+  std::vector<std::shared_ptr<Node>> pinned_;  // armed nodes, held from arm() to finalize
   std::vector<uintptr_t> keys_;
   bool active_ = false;
   std::vector<std::vector<int64_t>> dense_strides_;
@@ -202,6 +249,10 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
   std::vector<int32_t> ready_;
   void* stream_ = nullptr;
   bool in_backward_ = false, finalize_queued_ = false, record_order_ = false;
+  bool release_ = false;
+  std::vector<int> bucket_of_;
+  std::vector<std::vector<at::Tensor>> held_;
+  void* comm_stream_ = nullptr;
   std::vector<int> order_;
 };
 
@@ -215,12 +266,13 @@ variable_list MarkReady::operator()(const variable_list& outputs, const variable
 PYBIND11_MODULE(_gshook, m) {
   m.doc() = "libgsync DDP gradient hooks in C++ (AccumulateGrad post-hooks -> gs_bucketer_mark_ready)";
   py::class_<Hooks, std::shared_ptr<Hooks>>(m, "Hooks")
-      .def(py::init<std::vector<at::Tensor>, int, py::function>(), py::arg("params"), py::arg("device"),
-           py::arg("on_finalize"))
+      .def(py::init<std::vector<at::Tensor>, int, py::function, bool>(), py::arg("params"), py::arg("device"),
+           py::arg("on_finalize"), py::arg("release") = false)
       .def("attach", &Hooks::attach)
       .def("detach", &Hooks::detach)
       .def("attached", &Hooks::attached)
-      .def("set_bucketer", &Hooks::set_bucketer)
+      .def("set_bucketer", &Hooks::set_bucketer, py::arg("handle"), py::arg("n_buckets"),
+           py::arg("bucket_of") = std::vector<int>(), py::arg("comm_stream") = 0)
       .def("prepare", &Hooks::prepare)
       .def("order", &Hooks::order)
       .def("in_backward", &Hooks::in_backward)

@@ -266,10 +266,11 @@ class _Bucketer:
             pass
 
 
-def _make_native_hooks(ddp):
-    """The C++ hook object for `ddp` (None when GSYNC_NATIVE_HOOK=0 or the
-    extension is not built).  Its end-of-backward callback holds the DDP
-    weakly (the hooks live as long as the DDP, not the other way round)."""
+def _make_native_hooks(owner, params=None, release: bool = False):
+    """The C++ hook object for a DDP (or, `release`, a ZeRO engine) — None when
+    GSYNC_NATIVE_HOOK=0 or the extension is not built.  Its end-of-backward
+    callback holds the owner weakly (the hooks live as long as the owner, not
+    the other way round) and calls owner._native_finalized()."""
     if os.environ.get("GSYNC_NATIVE_HOOK", "1") == "0":
         return None
     mod = L.hook_module()
@@ -277,14 +278,14 @@ def _make_native_hooks(ddp):
         return None
     import weakref
 
-    ref = weakref.ref(ddp)
+    ref = weakref.ref(owner)
 
     def on_finalize():
         d = ref()
         if d is not None:
             d._native_finalized()
 
-    return mod.Hooks(ddp._params, ddp._dev_index, on_finalize)
+    return mod.Hooks(owner._params if params is None else params, owner._dev_index, on_finalize, release)
 
 
 class DistributedDataParallel(nn.Module, Joinable):

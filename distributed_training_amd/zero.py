@@ -127,13 +127,22 @@ class ZeroDataParallel:
         self.buckets = compute_bucket_assignment_by_size(self.params, [int(reduce_bucket_size) * esz], order=order)
         self._make_bucketer()
         self._build_flat_state()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.params)]
+        self._hooks = []
         self._in_backward = False
         self._queued = False
         self._pending = {}
         # [found_inf, Σg² (all-reduced), 1/scale, -, clip out: Σg²·s², coefficient, ‖g‖]
         self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
+        # the per-gradient hook in C++ (_gshook, release mode: the grad is freed once its
+        # pack is enqueued) on the library-collective path; Python hooks otherwise
+        from .ddp import _make_native_hooks
+
+        self._native = _make_native_hooks(self, self.params, release=True) if self._comm is not None else None
+        self._native_on = False
+        if self._native is not None:
+            self._native_bind()
+        self._set_native(self._native_ok())
 
     # ------------------------------------------------------------------ setup
     def _bcast(self, t):
@@ -222,8 +231,36 @@ class ZeroDataParallel:
             self.plan.set_ptrs(4, self.param_shards if self.lowp else [0] * len(shard_sizes))
 
     # ------------------------------------------------------------------ backward
+    # ---- which hooks run: C++ (_gshook) on the library-collective path, Python otherwise
+    def _native_ok(self) -> bool:
+        return self._native is not None and self._capture_local is None
+
+    def _native_bind(self):
+        self._native.set_bucketer(self.handle.value, len(self.buckets), [bi for bi, _ in self.loc],
+                                  self._comm.stream_ptr)
+
+    def _set_native(self, on: bool):
+        if on:
+            for h in self._hooks:
+                h.remove()
+            self._hooks = []
+            self._native.attach()
+        else:
+            if self._native is not None:
+                self._native.detach()
+            if not self._hooks:
+                self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                               for i, p in enumerate(self.params)]
+        self._native_on = on
+
+    def _native_finalized(self):
+        self._in_backward = False
+
     def prepare_backward(self):
         """Start a synchronising backward (called by the engine's backward())."""
+        want = self._native_ok()
+        if want != self._native_on:
+            self._set_native(want)
         if not self.require_backward_grad_sync:
             self._in_backward = False
             return
@@ -232,6 +269,8 @@ class ZeroDataParallel:
         self._queued = False
         self._pending = {}
         self._held = {}
+        if self._native_on:
+            self._native.prepare(False)
 
     def _make_hook(self, idx):
         def hook(param):
@@ -454,6 +493,12 @@ class ZeroDataParallel:
     def close(self):
         for h in self._hooks:
             h.remove()
+        self._hooks = []
+        nat = getattr(self, "_native", None)
+        if nat is not None:
+            nat.detach()
+            nat.set_bucketer(0, 0)
+            self._native_on = False
         if getattr(self, "handle", None) is not None and self.handle.value:
             L.destroy("gs_bucketer_destroy", self.handle)
             self.handle = None

@@ -88,3 +88,40 @@ def test_native_hooks_attach_detach():
     assert not h.attached()
     (p * 2).sum().backward()  # detached: nothing fires
     assert calls == [] and torch.equal(p.grad, torch.full((3,), 2.0))
+
+
+def _zero_native_vs_python(rank, ws):
+    """The ZeRO engine's release mode of the C++ hooks (grad freed once marked
+    ready, held until its bucket's pack is enqueued) on the host bucketer at
+    world size 1: weights after several AdamW steps with clipping equal the
+    Python-hook engine's bit for bit, and grads are released."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    res = []
+    for native in (True, False):
+        torch.manual_seed(0)
+        m = _micro()
+        eng = ZeroDataParallel(m, stage=2, optimizer="adamw", lr=1e-3, weight_decay=1e-2, gradient_clipping=0.5)
+        if native:
+            ref = weakref.ref(eng)
+            eng._native = L.hook_module().Hooks(eng.params, -1, lambda: ref()._native_finalized(), True)
+            eng._native.set_bucketer(eng.handle.value, len(eng.buckets), [bi for bi, _ in eng.loc], 0)
+            eng._native_ok = lambda: eng._capture_local is None
+        g = torch.Generator().manual_seed(3)
+        for it in range(4):
+            x = torch.rand(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            eng.prepare_backward()  # before the forward, as the engines call it
+            nn.functional.cross_entropy(m(x), y).backward()
+            assert all(p.grad is None for p in eng.params)  # released into the buckets
+            eng.step()
+        assert eng._native_on == native and not eng._in_backward
+        res.append([p.detach().clone() for p in m.parameters()])
+        eng.close()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_native_hooks_zero_release_mode_ws1():
+    _run(_zero_native_vs_python, 1)
