@@ -22,6 +22,7 @@
 #include <torch/csrc/autograd/variable.h>
 #include <torch/csrc/utils/pybind.h>
 
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 
 #include <algorithm>
@@ -195,8 +196,9 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
       if (comm_stream_ != nullptr) {
         // the pack on the comm stream is enqueued: the allocator may reuse these
         // grads' memory only after it has run
-        const c10::Stream cs = c10::hip::getStreamFromExternal(static_cast<hipStream_t>(comm_stream_),
-                                                                static_cast<c10::DeviceIndex>(device_));
+        // torch-ROCm's device type for GPU tensors is "cuda": the stream must say so too
+        const c10::Stream cs = c10::hip::getStreamFromExternalMasqueradingAsCUDA(
+            static_cast<hipStream_t>(comm_stream_), static_cast<c10::DeviceIndex>(device_));
         for (auto& t : hs) t.record_stream(cs);
       }
       hs.clear();
