@@ -88,7 +88,7 @@ def parse():
                     help="after the headline: BASELINE configs[4] (Colossal shim, ResNet-152 fp32 grads, fp16 "
                          "autocast, HybridAdam, 128 img/GPU) on the same ranks, the line's `colossal` object "
                          "(-1: at N > 1 on the DDP engine)")
-    ap.add_argument("--leg-budget-s", type=float, default=420.0,
+    ap.add_argument("--leg-budget-s", type=float, default=360.0,
                     help="N > 1: if the optional legs after the timed region (standalone collectives, parity, "
                          "policy A/B) overrun this, print the line with the legs done so far and end every rank "
                          "(0 = no watchdog)")
