@@ -948,6 +948,8 @@ def main():
         }
         if leg_errors:
             line["leg_errors"] = dict(leg_errors)
+        if leg_seconds:
+            line["leg_seconds"] = dict(leg_seconds)
         return line
 
     # ---- after the timed region.  The headline is complete here; what follows are
@@ -962,8 +964,11 @@ def main():
     leg_errors: dict = {}
     current_leg = ["start"]
 
+    leg_seconds: dict = {}
+
     def leg(name, fn):
         current_leg[0] = name
+        t_leg = time.perf_counter()
         try:
             return fn()
         except Exception as ex:  # recorded, the line still prints
@@ -972,6 +977,8 @@ def main():
             leg_errors[name] = repr(ex)
             print(f"[bench] leg {name} failed: {ex!r}\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             return None
+        finally:
+            leg_seconds[name] = round(time.perf_counter() - t_leg, 2)
 
     watchdog = None
     if world > 1 and args.leg_budget_s > 0:
