@@ -87,12 +87,11 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     if (on_finalize_ && Py_IsInitialized() && PyGILState_Check()) Py_DECREF(on_finalize_);
   }
 
-  // The hooks go on the AccumulateGrad nodes of each synchronising forward's
-  // graph (arm(), from prepare()), not on nodes created and pinned here: an
-  // AccumulateGrad runs on the stream that was current when it was created, so
-  // a node pinned at wrap time would accumulate on that stream even inside a
-  // later hipGraph capture on another one.  The variable holds its node
-  // weakly; the graph owns it and frees it, hook included, after backward.
+  // The hooks are armed per synchronising step (arm(), from prepare()), never
+  // on nodes pinned at wrap time: an AccumulateGrad runs on the stream that was
+  // current when it was created, so a node pinned at wrap time would
+  // accumulate on that stream even inside a later hipGraph capture on another
+  // one.  attach() / detach() switch the arming on and off.
   void attach() { active_ = true; }
 
   void detach() {
@@ -124,6 +123,7 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     finalize_queued_ = false;
     record_order_ = record_order;
     if (record_order) order_.clear();
+    for (auto& h : held_) h.clear();  // nothing held past a backward that did not finish
     if (active_) arm();
   }
 
