@@ -11,6 +11,8 @@ long as the GPU queue does not fill):
   torch_fused  torch DDP + torch.optim.Adam(fused=True)
   gsync        libgsync DDP + FusedAdam (GSYNC_NATIVE_HOOK decides the hook)
   nodpp        no DDP + FusedAdam (the floor for gradient-sync host cost)
+  colossal     the reference's Colossal step: Booster(TorchDDPPlugin, fp16) + HybridAdam (shim)
+  torch_amp    the same fp16 step on torch: DDP + autocast + GradScaler + torch.optim.Adam
 
     python scripts/cifar_host.py [--steps 100] [--out file.jsonl]
 """
@@ -59,6 +61,29 @@ def main():
             elif impl == "gsync":
                 ddp = D.DistributedDataParallel(model)
                 opt = D.FusedAdam(ddp.parameters(), lr=1e-3)
+            elif impl == "colossal":
+                # the reference's Colossal run (R:resnet/colossal/colossal_train.py:118-161,
+                # run.sh torch_ddp_fp16): Booster(TorchDDPPlugin, fp16) + HybridAdam on the shim
+                from distributed_training_amd.compat import colossalai as C
+
+                booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
+                hopt = C.HybridAdam(model.parameters(), lr=1e-3)
+                cmodel, copt, ccrit, _, _ = booster.boost(model, hopt, criterion=crit)
+                ddp = next(m for m in cmodel.modules() if isinstance(m, D.DistributedDataParallel))
+
+                class _Step:  # booster.backward + step, behind the loop's zero_grad/ddp/step calls
+                    def zero_grad(self, set_to_none=True):
+                        copt.zero_grad()
+
+                    def step(self):
+                        copt.step()
+
+                opt = _Step()
+            elif impl == "torch_amp":
+                # the same fp16 step on torch alone: DDP + autocast + GradScaler + torch.optim.Adam
+                ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
+                tadam = torch.optim.Adam(ddp.parameters(), lr=1e-3)
+                scaler = torch.amp.GradScaler("cuda")
             else:
                 ddp = model
                 opt = D.FusedAdam(model.parameters(), lr=1e-3)
@@ -67,14 +92,35 @@ def main():
             def one(acc):
                 pc = time.perf_counter
                 a = pc()
-                opt.zero_grad(set_to_none=True)
-                b = pc()
-                loss = crit(ddp(x), y)
-                c = pc()
-                loss.backward()
-                d = pc()
-                opt.step()
-                e = pc()
+                if impl == "torch_amp":
+                    tadam.zero_grad(set_to_none=True)
+                    b = pc()
+                    with torch.autocast("cuda", dtype=torch.float16):
+                        loss = crit(ddp(x), y)
+                    c = pc()
+                    scaler.scale(loss).backward()
+                    d = pc()
+                    scaler.step(tadam)
+                    scaler.update()
+                    e = pc()
+                elif impl == "colossal":
+                    opt.zero_grad()
+                    b = pc()
+                    loss = ccrit(cmodel(x), y)
+                    c = pc()
+                    booster.backward(loss, copt)
+                    d = pc()
+                    opt.step()
+                    e = pc()
+                else:
+                    opt.zero_grad(set_to_none=True)
+                    b = pc()
+                    loss = crit(ddp(x), y)
+                    c = pc()
+                    loss.backward()
+                    d = pc()
+                    opt.step()
+                    e = pc()
                 if acc:
                     t["zero"] += b - a
                     t["fwd"] += c - b
@@ -105,7 +151,7 @@ def main():
             if out:
                 out.write(json.dumps(row) + "\n")
                 out.flush()
-            del ddp, opt, model
+            del ddp, model
     dist.destroy_process_group()
 
 
