@@ -986,7 +986,16 @@ def main():
 
         def expire():
             if rank == 0:
-                ln = make_line()
+                try:
+                    ln = make_line()
+                except Exception as ex:  # the headline alone, whatever else failed
+                    ln = {"metric": "images/sec (node) ResNet-50 at 1/2/4/8 MI355X; grad-sync bus GB/s",
+                          "value": img_s, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+                          "config": {"workload": f"{args.model} synthetic 224x224 training, {args.batch} img/GPU",
+                                     "parallelism": f"dp{world}", "global_batch": args.batch * world},
+                          "line_error": repr(ex)}
                 ln["legs_incomplete"] = {"leg": current_leg[0], "budget_s": args.leg_budget_s}
                 print(json.dumps(ln), flush=True)
             print(f"[bench] rank {rank}: legs overran {args.leg_budget_s}s in {current_leg[0]}: exiting",
