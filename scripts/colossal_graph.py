@@ -1,0 +1,80 @@
+"""Probe: the reference's Colossal fp16 CIFAR step (Booster(TorchDDPPlugin,
+fp16) + HybridAdam, R:resnet/colossal/colossal_train.py:97-102,118-161) recorded
+as one hipGraph with CapturedStep — the GradScaler path is device-only (the
+inf check inside the DDP unpack, the update kernels skip on the device flag,
+the scale update on the device), so the whole step can be replayed.  Eager vs
+graph: losses over the same batches and ms/step.
+
+    python scripts/colossal_graph.py [--steps 60]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--batch", type=int, default=100)
+    args = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29619")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import distributed_training_amd as D
+    from distributed_training_amd.compat import colossalai as C
+    from distributed_training_amd.resnet import MODELS
+
+    torch.backends.cudnn.deterministic = True
+    g = torch.Generator(device=dev).manual_seed(1)
+    xs = [torch.rand(args.batch, 3, 32, 32, device=dev, generator=g) for _ in range(8)]
+    ys = [torch.randint(0, 10, (args.batch,), device=dev, generator=g) for _ in range(8)]
+    res = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = MODELS["resnet18"](num_classes=10).to(dev)
+        booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
+        opt = C.HybridAdam(model.parameters(), lr=1e-3)
+        if mode == "graph":
+            opt.defaults["capturable"] = True  # device step counters / lr (FusedAdam capturable)
+        cmodel, copt, ccrit, _, _ = booster.boost(model, opt, criterion=nn.CrossEntropyLoss())
+
+        def step(x, y):
+            copt.zero_grad()
+            loss = ccrit(cmodel(x), y)
+            booster.backward(loss, copt)
+            copt.step()
+            return loss.detach()
+
+        run = D.CapturedStep(step, optimizers=[opt], warmup=3) if mode == "graph" else step
+        losses = []
+        for i in range(12):
+            losses.append(float(run(xs[i % 8], ys[i % 8])))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            run(xs[i % 8], ys[i % 8])
+            torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        res[mode] = {"losses": losses, "ms_per_step": ms,
+                     "captures": getattr(run, "captures", None), "replays": getattr(run, "replays", None)}
+        print(json.dumps({"mode": mode, **res[mode]}), flush=True)
+    le, lg = res["eager"]["losses"], res["graph"]["losses"]
+    print(json.dumps({"max_loss_diff": max(abs(a - b) for a, b in zip(le, lg)),
+                      "speedup": res["eager"]["ms_per_step"] / res["graph"]["ms_per_step"]}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

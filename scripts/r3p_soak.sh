@@ -12,3 +12,6 @@ for f in ("gpurun_out/r3p_soak_r50.json", "gpurun_out/r3p_soak_r18.json"):
     print(f, round(d["value"], 1), round(d["ms_per_step"], 3), d["parity"]["ok"], round(d["roofline"]["frac"], 3),
           d["memory"]["max_allocated_GB"])
 PY
+# probe: the Colossal fp16 CIFAR step as one hipGraph
+timeout -k 10 300 python -u scripts/colossal_graph.py --steps 60 > $OUT/r3p_colossal_graph.jsonl 2> $OUT/r3p_colossal_graph.err || { tail -20 $OUT/r3p_colossal_graph.err; exit 1; }
+cat $OUT/r3p_colossal_graph.jsonl
