@@ -82,7 +82,9 @@ class HybridAdam(FusedAdam):
                  weight_decay=0.0, adamw_mode=True, nvme_offload_fraction=0.0, nvme_offload_dir=None, **kw):
         if not bias_correction:
             raise NotImplementedError("bias_correction=False")
-        super().__init__(model_params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=adamw_mode)
+        # capturable (not a Colossal argument): device step counters / lr, for CapturedStep
+        super().__init__(model_params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=adamw_mode,
+                         capturable=bool(kw.pop("capturable", False)))
         self.colossal_kwargs = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw_mode=adamw_mode)
 
 

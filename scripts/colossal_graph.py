@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--deterministic", type=int, default=1,
+                    help="1: deterministic MIOpen (losses comparable bit for bit); 0: the default kernels (timing)")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29619")
@@ -36,7 +38,7 @@ def main():
     from distributed_training_amd.compat import colossalai as C
     from distributed_training_amd.resnet import MODELS
 
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     g = torch.Generator(device=dev).manual_seed(1)
     xs = [torch.rand(args.batch, 3, 32, 32, device=dev, generator=g) for _ in range(8)]
     ys = [torch.randint(0, 10, (args.batch,), device=dev, generator=g) for _ in range(8)]
@@ -45,9 +47,7 @@ def main():
         torch.manual_seed(0)
         model = MODELS["resnet18"](num_classes=10).to(dev)
         booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
-        opt = C.HybridAdam(model.parameters(), lr=1e-3)
-        if mode == "graph":
-            opt.defaults["capturable"] = True  # device step counters / lr (FusedAdam capturable)
+        opt = C.HybridAdam(model.parameters(), lr=1e-3, capturable=mode == "graph")
         cmodel, copt, ccrit, _, _ = booster.boost(model, opt, criterion=nn.CrossEntropyLoss())
 
         def step(x, y):
@@ -71,7 +71,7 @@ def main():
                      "captures": getattr(run, "captures", None), "replays": getattr(run, "replays", None)}
         print(json.dumps({"mode": mode, **res[mode]}), flush=True)
     le, lg = res["eager"]["losses"], res["graph"]["losses"]
-    print(json.dumps({"max_loss_diff": max(abs(a - b) for a, b in zip(le, lg)),
+    print(json.dumps({"deterministic": bool(args.deterministic), "max_loss_diff": max(abs(a - b) for a, b in zip(le, lg)),
                       "speedup": res["eager"]["ms_per_step"] / res["graph"]["ms_per_step"]}), flush=True)
     dist.destroy_process_group()
 

@@ -151,3 +151,50 @@ def test_captured_ddp_step_tracks_eager(cuda_device, rccl_pg, opt_name, set_to_n
     assert all(abs(a - b) <= 1e-3 * max(1.0, abs(a)) for a, b in zip(le, lg)), (le, lg)
     for a, b in zip(pe, pg):
         torch.testing.assert_close(b, a, rtol=1e-3, atol=1e-4)
+
+
+def test_captured_colossal_fp16_step_equals_eager(cuda_device, rccl_pg):
+    """The reference's Colossal fp16 step (Booster(TorchDDPPlugin, fp16) +
+    HybridAdam, R:resnet/colossal/colossal_train.py:97-102,118-161) recorded as
+    one hipGraph: the GradScaler path is device-only (inf check in the DDP
+    unpack, update kernels skip on the device flag, scale update on the device),
+    so the replayed losses equal the eager ones bit for bit (deterministic
+    MIOpen)."""
+    import torch.nn as nn
+
+    import distributed_training_amd as D
+    from distributed_training_amd.compat import colossalai as C
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    gen = torch.Generator(device=cuda_device).manual_seed(5)
+    xs = [torch.rand(16, 3, 32, 32, device=cuda_device, generator=gen) for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device=cuda_device, generator=gen) for _ in range(4)]
+    runs = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = micro_resnet().to(cuda_device)
+        booster = C.Booster(plugin=C.TorchDDPPlugin(), mixed_precision="fp16")
+        opt = C.HybridAdam(model.parameters(), lr=1e-3, capturable=mode == "graph")
+        cmodel, copt, ccrit, _, _ = booster.boost(model, opt, criterion=nn.CrossEntropyLoss())
+
+        def step(x, y):
+            copt.zero_grad()
+            loss = ccrit(cmodel(x), y)
+            booster.backward(loss, copt)
+            copt.step()
+            return loss.detach()
+
+        run = D.CapturedStep(step, optimizers=[opt], warmup=3) if mode == "graph" else step
+        losses = [float(run(xs[i % 4], ys[i % 4])) for i in range(10)]
+        torch.cuda.synchronize()
+        if mode == "graph":
+            assert run.captures == 1 and run.replays == 6
+        runs[mode] = (losses, [p.detach().clone() for p in model.parameters()])
+        for m in cmodel.modules():
+            if isinstance(m, D.DistributedDataParallel):
+                m.close()
+    assert runs["eager"][0] == runs["graph"][0]
+    for a, b in zip(runs["eager"][1], runs["graph"][1]):
+        assert torch.equal(a, b)
