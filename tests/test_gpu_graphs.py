@@ -190,7 +190,7 @@ def test_captured_colossal_fp16_step_equals_eager(cuda_device, rccl_pg):
         losses = [float(run(xs[i % 4], ys[i % 4])) for i in range(10)]
         torch.cuda.synchronize()
         if mode == "graph":
-            assert run.captures == 1 and run.replays == 6
+            assert run.captures == 1 and run.replays == 7  # every call after the warm-up replays
         runs[mode] = (losses, [p.detach().clone() for p in model.parameters()])
         for m in cmodel.modules():
             if isinstance(m, D.DistributedDataParallel):
