@@ -54,7 +54,8 @@ def _hyper_key(optimizers):
     which they read from device memory)."""
     key = []
     for opt in optimizers:
-        skip = ("params", "lr") if isinstance(opt, _FusedBase) else ("params",)
+        # libgsync optimizers and the capturable ZeRO engine read lr from device memory
+        skip = ("params", "lr") if (isinstance(opt, _FusedBase) or hasattr(opt, "refresh_hyper")) else ("params",)
         for g in opt.param_groups:
             key.append(tuple(sorted((k, repr(v)) for k, v in g.items() if k not in skip)))
             key.append(tuple(id(p) for p in g["params"]))
@@ -65,7 +66,7 @@ class CapturedStep:
     def __init__(self, step_fn: Callable, optimizers: Sequence[torch.optim.Optimizer] = (), warmup: int = 3,
                  pool=None):
         for opt in optimizers:
-            if isinstance(opt, _FusedBase) and not opt.capturable:
+            if (isinstance(opt, _FusedBase) or hasattr(opt, "refresh_hyper")) and not getattr(opt, "capturable", True):
                 raise ValueError(f"{type(opt).__name__} must be created with capturable=True to be recorded")
         self.step_fn = step_fn
         self.optimizers = list(optimizers)
@@ -84,7 +85,7 @@ class CapturedStep:
     # ------------------------------------------------------------------ helpers
     def _refresh(self):
         for opt in self.optimizers:
-            if isinstance(opt, _FusedBase):
+            if isinstance(opt, _FusedBase) or hasattr(opt, "refresh_hyper"):
                 opt.refresh_hyper()
 
     def _signature(self, args):

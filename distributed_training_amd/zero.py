@@ -83,7 +83,8 @@ class ZeroDataParallel:
     def __init__(self, module: torch.nn.Module, *, stage: int = 2, optimizer: str = "adamw", lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.0,
                  process_group=None, reduce_bucket_size: int = int(5e7), gradient_clipping: float = 0.0,
-                 loss_scaler: DynamicLossScaler | None = None, broadcast_params: bool = True):
+                 loss_scaler: DynamicLossScaler | None = None, broadcast_params: bool = True,
+                 capturable: bool = False):
         if stage not in (1, 2):
             raise NotImplementedError(f"ZeRO stage {stage}: only 1 and 2 are on the gradient-sync path")
         if not dist.is_initialized():
@@ -107,6 +108,12 @@ class ZeroDataParallel:
         self.clip = float(gradient_clipping or 0.0)
         self.scaler = loss_scaler
         self.step_count = 0
+        # capturable (CapturedStep): Adam's step counter, lr and bias corrections live on
+        # the device (gs_adam_hyper advances them per launch, also on graph replays)
+        self.capturable = bool(capturable)
+        if self.capturable and (loss_scaler is not None or optimizer == "sgd"):
+            raise NotImplementedError("capturable ZeRO: Adam/AdamW without a dynamic loss scaler "
+                                      "(DeepSpeed's overflow check reads the flag on the host)")
         self.require_backward_grad_sync = True
         backend = dist.get_backend(self.pg)
         self._comm = None
@@ -374,6 +381,17 @@ class ZeroDataParallel:
         if self.kind == "sgd":
             self.plan.sgd(self.dtype, g0["lr"], g0["momentum"], 0.0, g0["weight_decay"], False, False,
                           self.step_count == 1, lowp_dtype=lowp, grad_scale=grad_scale, found_inf=found_inf)
+        elif self.capturable:
+            # device hyper-parameters: advance the step, form [step_size, bc2_sqrt, 1 - lr*wd]
+            # (the same double arithmetic as the host branch, T:optim/adam.py), the kernel reads them
+            b1, b2 = g0["betas"]
+            h = self._hyper_state()
+            L.check(L.lib().gs_adam_hyper(L.GS_DEV_HIP if self.is_cuda else L.GS_DEV_HOST, h["step"].data_ptr(),
+                                          h["lr"].data_ptr(), float(b1), float(b2), float(g0["weight_decay"]), None,
+                                          h["hyper"].data_ptr(), L.stream_ptr(self.device) if self.is_cuda else None),
+                    "gs_adam_hyper")
+            self.plan.adam(self.dtype, g0["lr"], b1, b2, g0["eps"], g0["weight_decay"], self.kind == "adamw", False,
+                           -1.0, 1.0, lowp_dtype=lowp, grad_scale=grad_scale, found_inf=found_inf)
         else:
             b1, b2 = g0["betas"]
             bc1 = 1 - b1 ** self.step_count
@@ -392,6 +410,33 @@ class ZeroDataParallel:
             self.scaler.update(overflow)
         return not overflow
 
+    def _hyper_state(self):
+        """Device step counter (fp64), lr (fp64) and the kernel's hyper source
+        (fp32 [step_size, bc2_sqrt, 1 - lr*wd]) of the capturable mode."""
+        h = getattr(self, "_dev_hyper", None)
+        if h is None:
+            h = self._dev_hyper = {
+                "step": torch.full((1,), float(self.step_count - 1), dtype=torch.float64, device=self.device),
+                "lr": torch.full((1,), float(self.param_groups[0]["lr"]), dtype=torch.float64, device=self.device),
+                "hyper": torch.zeros(3, dtype=torch.float32, device=self.device), "lr_host": self.param_groups[0]["lr"]}
+            self.plan.set_hyper_source(h["hyper"])
+        return h
+
+    def refresh_hyper(self):
+        """Write a changed host lr (a WarmupLR step) into the device buffer —
+        outside a capture; CapturedStep calls it before every replay."""
+        h = getattr(self, "_dev_hyper", None)
+        lr = self.param_groups[0]["lr"]
+        if h is not None and h["lr_host"] != lr:
+            h["lr"].fill_(float(lr))
+            h["lr_host"] = lr
+
+    def device_step_count(self) -> int:
+        """The step count (capturable: read from the device counter, which graph
+        replays advance; a host read)."""
+        h = getattr(self, "_dev_hyper", None)
+        return int(h["step"].item()) if h is not None else self.step_count
+
     def zero_grad(self, set_to_none=True):
         for p in self.params:
             p.grad = None
@@ -403,7 +448,7 @@ class ZeroDataParallel:
     def state_dict(self):
         """This rank's optimizer shard (fp32 master + states): DeepSpeed's
         zero_pp_rank_<r>_mp_rank_00_optim_states layout, one file per rank."""
-        return {"step": self.step_count, "rank": self.rank, "world": self.world, "stage": self.stage,
+        return {"step": self.device_step_count(), "rank": self.rank, "world": self.world, "stage": self.stage,
                 "bucket_numel": list(self.bucket_numel), "kind": self.kind,
                 "master": [m.detach().float().cpu().clone() for m in self.master],
                 "exp_avg": [t.cpu() for t in self.state1], "exp_avg_sq": [t.cpu() for t in self.state2],
@@ -418,6 +463,7 @@ class ZeroDataParallel:
                                f"{sd['bucket_numel']}; this engine is rank {self.rank}/{self.world} with "
                                f"{self.bucket_numel}")
         self.step_count = int(sd["step"])
+        self._dev_hyper = None  # re-derived from the loaded step count on the next step
         for m, v in zip(self.master, sd["master"]):
             m.copy_(v.to(m.device, m.dtype))
         for t, v in zip(self.state1, sd["exp_avg"]):

@@ -198,3 +198,53 @@ def test_captured_colossal_fp16_step_equals_eager(cuda_device, rccl_pg):
     assert runs["eager"][0] == runs["graph"][0]
     for a, b in zip(runs["eager"][1], runs["graph"][1]):
         assert torch.equal(a, b)
+
+
+def test_captured_zero2_step_equals_eager(cuda_device, rccl_pg):
+    """The reference's DeepSpeed step shape (bf16 model, ZeRO-2, AdamW, clip 1.0,
+    R:resnet/deepspeed/deepspeed_train.py:170-219) on ZeroDataParallel(capturable=True)
+    recorded as one hipGraph — C++ hooks in release mode, reduce-scatter, folded
+    clip, device Adam hyper-parameters, all-gather — with an lr schedule stepped
+    outside the graph: losses and fp32 master shards equal the eager engine's
+    bit for bit (deterministic MIOpen)."""
+    import distributed_training_amd as D
+    from distributed_training_amd.resnet import micro_resnet
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    gen = torch.Generator(device=cuda_device).manual_seed(5)
+    xs = [torch.rand(16, 3, 32, 32, device=cuda_device, generator=gen).to(torch.bfloat16) for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device=cuda_device, generator=gen) for _ in range(4)]
+    crit = torch.nn.CrossEntropyLoss()
+    runs = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = micro_resnet().to(cuda_device).to(torch.bfloat16)
+        eng = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=1e-3, weight_decay=3e-7,
+                               gradient_clipping=1.0, capturable=True)
+
+        def step(x, y):
+            eng.prepare_backward()
+            loss = crit(model(x).float(), y)
+            loss.backward()
+            eng.step()
+            eng.zero_grad()
+            return loss.detach()
+
+        run = D.CapturedStep(step, optimizers=[eng], warmup=3) if mode == "graph" else step
+        losses = []
+        for i in range(10):
+            eng.param_groups[0]["lr"] = 1e-3 * min(1.0, (i + 1) / 5)  # warm-up, stepped outside
+            if mode == "eager":
+                eng.refresh_hyper()
+            losses.append(float(run(xs[i % 4], ys[i % 4])))
+        torch.cuda.synchronize()
+        if mode == "graph":
+            assert run.captures == 1 and run.replays == 7
+        assert eng.device_step_count() == 10
+        runs[mode] = (losses, [m.detach().clone() for m in eng.master])
+        eng.close()
+    assert runs["eager"][0] == runs["graph"][0]
+    for a, b in zip(runs["eager"][1], runs["graph"][1]):
+        assert torch.equal(a, b)

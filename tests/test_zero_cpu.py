@@ -114,3 +114,40 @@ def _zero_overflow(rank, ws, device="cpu", dtype=torch.float32):
 
 def test_zero2_dynamic_loss_scaling_overflow_skip_ws2():
     _run(_zero_overflow, 2)
+
+
+def _zero_capturable(rank, ws):
+    """capturable=True (device step counter, lr and bias corrections through
+    gs_adam_hyper, the kernel reading them) equals the host-hyper engine bit
+    for bit over steps with lr changes (refresh_hyper) and clipping; the device
+    step count is the truth for state_dict."""
+    from tests.test_ddp_cpu import _micro
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    res = []
+    for capt in (False, True):
+        torch.manual_seed(0)
+        m = _micro().to(torch.bfloat16)
+        eng = ZeroDataParallel(m, stage=2, optimizer="adamw", lr=1e-3, weight_decay=1e-2, gradient_clipping=0.5,
+                               capturable=capt)
+        g = torch.Generator().manual_seed(7 + rank)
+        for it in range(5):
+            eng.param_groups[0]["lr"] = 1e-3 * (1 + it)  # a warm-up schedule, stepped by the caller
+            eng.refresh_hyper()
+            x = torch.rand(4, 3, 32, 32, generator=g).to(torch.bfloat16)
+            y = torch.randint(0, 10, (4,), generator=g)
+            eng.prepare_backward()
+            torch.nn.functional.cross_entropy(m(x).float(), y).backward()
+            eng.step()
+            eng.zero_grad()
+        assert eng.state_dict()["step"] == 5
+        res.append([t.detach().clone() for t in eng.master] + [t.clone() for t in eng.state1 + eng.state2])
+        eng.close()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_zero_capturable_equals_host_hyper_ws2():
+    from tests.test_ddp_cpu import _run
+
+    _run(_zero_capturable, 2)
