@@ -52,3 +52,8 @@ def test_bench_rccl_parity_multi_gpu(engine):
     g = lines[0]["grad_sync"]
     if engine == "ddp":
         assert g["allreduce_bus_GBps"] > 0 and g["xgmi_peak_GBps"] == (N - 1) * 153.0
+        # the same run times BASELINE configs[3] and [4] on its ranks (bench.py legs)
+        for leg in ("zero2", "colossal"):
+            assert lines[0][leg]["parity"]["ok"] is True, (leg, lines[0][leg]["parity"])
+            assert lines[0][leg]["parity"]["collective"] == "rccl(libgsync)"
+        assert "leg_errors" not in lines[0], lines[0].get("leg_errors")
