@@ -300,14 +300,20 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     import distributed_training_amd as D
     from distributed_training_amd import parity as PC
 
-    variants = [("torch", {}), ("xgmi", {"bucket_policy": "xgmi"}),
-                ("last_bucket_cap_1MiB", {"last_bucket_cap_mb": 1.0}), ("torch_again", {})]
     bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
+    # bf16_buckets: half the bytes on the links, but other numerics (opt-in) — reported,
+    # never a candidate for the default
+    variants = [("torch", {}), ("xgmi", {"bucket_policy": "xgmi"}),
+                ("last_bucket_cap_1MiB", {"last_bucket_cap_mb": 1.0}),
+                *([("bf16_buckets", {"bucket_dtype": torch.bfloat16})] if bucket_dtype is None else []),
+                ("torch_again", {})]
     ddp.close()
     peak = (world - 1) * XGMI_LINK_GBPS
     rows = {}
     for name, kw in variants:
-        v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bucket_dtype,
+        kw = dict(kw)
+        bdt = kw.pop("bucket_dtype", bucket_dtype)
+        v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bdt,
                                       gradient_as_bucket_view=args.grad_as_bucket_view, **kw)
 
         def fwd_bwd():
@@ -359,6 +365,8 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
         v.close()
     base = (rows["torch"]["images_per_sec"] + rows["torch_again"]["images_per_sec"]) / 2
     best, best_ips = "torch", base * (1 + POLICY_MARGIN)
+    if "bf16_buckets" in rows:
+        rows["bf16_buckets"]["vs_torch"] = rows["bf16_buckets"]["images_per_sec"] / base
     for name in ("xgmi", "last_bucket_cap_1MiB"):
         r = rows[name]
         r["vs_torch"] = r["images_per_sec"] / base
@@ -366,7 +374,8 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
             best, best_ips = name, r["images_per_sec"]
     return {"variants": rows, "steps_each": steps, "torch_mean_images_per_sec": base,
             "rule": f"a variant becomes the default if images/s >= (1 + {POLICY_MARGIN}) x the mean of the two "
-                    "torch-layout runs with parity.ok (DESIGN §8); best such variant wins",
+                    "torch-layout runs with parity.ok (DESIGN §8); best such variant wins; bf16_buckets is "
+                    "reported only (other numerics)",
             "decision": best}
 
 
