@@ -306,6 +306,7 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     variants = [("torch", {}), ("xgmi", {"bucket_policy": "xgmi"}),
                 ("last_bucket_cap_1MiB", {"last_bucket_cap_mb": 1.0}),
                 *([("bf16_buckets", {"bucket_dtype": torch.bfloat16})] if bucket_dtype is None else []),
+                ("rccl_cta_cap_16", {"rccl_max_ctas": 16}),
                 ("torch_again", {})]
     ddp.close()
     peak = (world - 1) * XGMI_LINK_GBPS
@@ -367,7 +368,7 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     best, best_ips = "torch", base * (1 + POLICY_MARGIN)
     if "bf16_buckets" in rows:
         rows["bf16_buckets"]["vs_torch"] = rows["bf16_buckets"]["images_per_sec"] / base
-    for name in ("xgmi", "last_bucket_cap_1MiB"):
+    for name in ("xgmi", "last_bucket_cap_1MiB", "rccl_cta_cap_16"):
         r = rows[name]
         r["vs_torch"] = r["images_per_sec"] / base
         if r["parity"] and r["parity"].get("ok") and r["images_per_sec"] >= best_ips:

@@ -65,6 +65,7 @@ SIGNATURES = {
     "gs_comm_unique_id_bytes": (_c_int, []),
     "gs_comm_get_unique_id": (_c_int, [_p_u8]),
     "gs_comm_create": (_c_int, [_c_int, _c_int, _p_u8, _c_int, _p_vp]),
+    "gs_comm_create_ex": (_c_int, [_c_int, _c_int, _p_u8, _c_int, _c_int, _p_vp]),
     "gs_comm_destroy": (_c_int, [_vp]),
     "gs_comm_abort": (_c_int, [_vp]),
     "gs_comm_set_timeout": (_c_int, [_vp, _c_i64]),

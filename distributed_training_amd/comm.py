@@ -25,7 +25,8 @@ DEFAULT_TIMEOUT_MS = 600_000  # torch's default process-group timeout (10 min)
 
 
 class Communicator:
-    def __init__(self, process_group=None, device: torch.device | None = None, timeout_ms: int | None = None):
+    def __init__(self, process_group=None, device: torch.device | None = None, timeout_ms: int | None = None,
+                 max_ctas: int = 0):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         if device.type != "cuda":
@@ -42,7 +43,9 @@ class Communicator:
         uid = (ctypes.c_uint8 * nbytes).from_buffer_copy(self._exchange_uid(bytes(uid)))
         h = ctypes.c_void_p()
         torch.cuda.set_device(device)
-        L.check(lib.gs_comm_create(self.rank, self.world, uid, device.index, ctypes.byref(h)), "gs_comm_create")
+        self.max_ctas = int(max_ctas)
+        L.check(lib.gs_comm_create_ex(self.rank, self.world, uid, device.index, self.max_ctas, ctypes.byref(h)),
+                "gs_comm_create_ex")
         self.handle = h
         import weakref
 

@@ -228,6 +228,10 @@ int gs_comm_get_unique_id(uint8_t* out) {
 }
 
 int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm** out) {
+  return gs_comm_create_ex(rank, world, uid, device, 0, out);
+}
+
+int gs_comm_create_ex(int rank, int world, const uint8_t* uid, int device, int max_ctas, gs_comm** out) {
   GS_CHECK_ARG(out && uid, "gs_comm_create: NULL argument");
   GS_CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "gs_comm_create: bad rank/world");
   if (hip_device_count() <= device) return fail(GS_ENODEV, "gs_comm_create: no HIP device");
@@ -245,7 +249,15 @@ int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm*
   }
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
-  ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+  ncclResult_t r;
+  if (max_ctas > 0) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.maxCTAs = max_ctas;
+    cfg.minCTAs = 1;
+    r = ncclCommInitRankConfig(&c->comm, world, id, rank, &cfg);
+  } else {
+    r = ncclCommInitRank(&c->comm, world, id, rank);
+  }
   if (r != ncclSuccess) {
     (void)hipStreamDestroy(c->stream);
     delete c;

@@ -294,7 +294,8 @@ class DistributedDataParallel(nn.Module, Joinable):
                  check_reduction=False, gradient_as_bucket_view=False, static_graph=False,
                  delay_all_reduce_named_params=None, param_to_hook_all_reduce=None, mixed_precision=None,
                  device_mesh=None, skip_all_reduce_unused_params=False, *, bucket_dtype=None,
-                 collective: str = "auto", bucket_policy: str = "torch", last_bucket_cap_mb=None):
+                 collective: str = "auto", bucket_policy: str = "torch", last_bucket_cap_mb=None,
+                 rccl_max_ctas: int | None = None):
         super().__init__()
         Joinable.__init__(self)  # the join config (disabled until a Join context enables it)
         self._divide_by_initial_world_size = True
@@ -360,9 +361,18 @@ class DistributedDataParallel(nn.Module, Joinable):
 
         # library-owned RCCL communicator for CUDA tensors over an nccl (=RCCL) group
         self._comm = None
+        self._own_comm = False
         if self.device.type == "cuda" and collective != "process_group" and self._backend == "nccl":
-            self._comm = get_communicator(None if self.process_group is dist.group.WORLD else self.process_group,
-                                          torch.device("cuda", self._dev_index))
+            pg = None if self.process_group is dist.group.WORLD else self.process_group
+            if rccl_max_ctas:
+                # RCCL's per-collective workgroup cap (ncclConfig_t maxCTAs): a communicator
+                # of this DDP's own, closed with it (the shared one keeps RCCL's default)
+                from .comm import Communicator
+
+                self._comm = Communicator(pg, torch.device("cuda", self._dev_index), max_ctas=int(rccl_max_ctas))
+                self._own_comm = True
+            else:
+                self._comm = get_communicator(pg, torch.device("cuda", self._dev_index))
         self._comm_hook: tuple[Any, Callable] | None = None
         self._buffers_plan = None
         self._sqnorm_target: torch.Tensor | None = None
@@ -1196,6 +1206,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             "bucket_dtype": str(self._bucket_dtype) if self._bucket_dtype is not None else
             ",".join(sorted({str(d) for d in b.bucket_dtypes})),
             "bucket_policy": self.bucket_policy,
+            "rccl_max_ctas": self._comm.max_ctas if self._comm is not None else None,
             "last_bucket_cap_bytes": self._last_bucket_cap,
             "xgmi_calibration": self._xgmi_calibration,
             "num_parameter_tensors": len(self._params),
@@ -1315,6 +1326,9 @@ class DistributedDataParallel(nn.Module, Joinable):
                     if p.grad is not None:
                         p.grad = p.grad.clone()
             b.close()
+        if getattr(self, "_own_comm", False) and self._comm is not None:
+            self._comm.close()
+            self._own_comm = False
 
     def __del__(self):
         for h in getattr(self, "_hook_handles", []):

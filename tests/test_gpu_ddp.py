@@ -165,6 +165,35 @@ def test_ddp_bf16_bucket_ws1(cuda_device, rccl_pg):
         assert np.array_equal(to_np(p.grad).reshape(-1), want)
 
 
+def test_ddp_rccl_max_ctas_ws1(cuda_device, rccl_pg):
+    """rccl_max_ctas: the DDP owns a communicator built with ncclConfig_t
+    maxCTAs; grads stay the local grads (ws=1, x*1.0 exact) and close() frees it."""
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd.comm import get_communicator
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.manual_seed(0)
+    model = micro_resnet().to(cuda_device)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model, rccl_max_ctas=4)
+    assert ddp._own_comm and ddp._comm.max_ctas == 4
+    assert ddp._comm is not get_communicator(None, cuda_device)
+    assert ddp._get_ddp_logging_data()["rccl_max_ctas"] == 4
+    x = torch.rand(8, 3, 32, 32, device=cuda_device)
+    for _ in range(2):
+        for p in params:
+            p.grad = None
+        ddp(x).sum().backward()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            assert torch.equal(p.grad, local[i])
+    comm = ddp._comm
+    ddp.close()
+    assert not ddp._own_comm and comm.handle is None
+
+
 def _ws2_worker(rank, ws, port, errq):
     try:
         import distributed_training_amd as D

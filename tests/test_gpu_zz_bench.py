@@ -122,7 +122,8 @@ def _check_policy_ab(d, n):
     """The bucket-policy A/B the driver's N>1 run carries (DESIGN §8's rule
     decides row N1 from it): every variant timed, parity-checked, with its tail."""
     ab = d["bucket_policy_ab"]
-    assert set(ab["variants"]) == {"torch", "xgmi", "last_bucket_cap_1MiB", "bf16_buckets", "torch_again"}
+    assert set(ab["variants"]) == {"torch", "xgmi", "last_bucket_cap_1MiB", "bf16_buckets", "rccl_cta_cap_16",
+                                   "torch_again"}
     assert ab["decision"] != "bf16_buckets"
     for name, r in ab["variants"].items():
         assert r["images_per_sec"] > 0 and r["ms_per_step"] > 0, name
