@@ -1,0 +1,10 @@
+#!/bin/bash
+# RCCL CTA cap: the DDP GPU test, the bench contract module (A/B with the
+# rccl_cta_cap_16 variant) and one N=1 bench line
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+timeout -k 10 1100 python -u -m pytest tests/test_gpu_ddp.py tests/test_gpu_zz_bench.py -m gpu -x -v --timeout 700 --timeout-method thread > $OUT/r3v_pytest.log 2>&1
+rc=$?; tail -3 $OUT/r3v_pytest.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/r3v_bench.json 2> $OUT/r3v_bench.err
+rc=$?; tail -c 400 $OUT/r3v_bench.json; exit $rc
