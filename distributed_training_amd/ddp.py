@@ -33,6 +33,8 @@ import ctypes
 import os
 import sys
 from contextlib import contextmanager
+from dataclasses import dataclass
+from enum import Enum, auto
 from typing import Any, Callable
 
 import torch
@@ -266,6 +268,19 @@ class _Bucketer:
             pass
 
 
+class _BufferCommHookLocation(Enum):
+    """Where a buffer comm hook runs (T:nn/parallel/distributed.py:226-228)."""
+    PRE_FORWARD = auto()
+    POST_FORWARD = auto()
+
+
+@dataclass
+class _BufferCommHook:
+    buffer_comm_hook: Callable
+    buffer_comm_hook_state: Any
+    buffer_comm_hook_location: _BufferCommHookLocation
+
+
 def _make_native_hooks(owner, params=None, release: bool = False):
     """The C++ hook object for a DDP (or, `release`, a ZeRO engine) — None when
     GSYNC_NATIVE_HOOK=0 or the extension is not built.  Its end-of-backward
@@ -325,6 +340,8 @@ class DistributedDataParallel(nn.Module, Joinable):
         # minus the names _set_params_and_buffers_to_ignore_for_model listed (torch's
         # ``parameters_to_ignore``: neither synchronised nor broadcast)
         self.parameters_to_ignore = set(getattr(module, "_ddp_params_and_buffers_to_ignore", ()))
+        self.buffer_hook = None  # _register_buffer_comm_hook
+        self._post_bwd_futs = []
         seen = set()
         self._params, self._param_names = [], []
         for name, p in module.named_parameters():
@@ -494,6 +511,8 @@ class DistributedDataParallel(nn.Module, Joinable):
         the Python side of _finalize_backward (once per backward)."""
         if self._record_order:
             self._ready_order = list(self._native.order())
+        if self._post_bwd_futs:
+            self._wait_post_backward_futures()
         self._found_inf_valid = self._found_inf_target is not None
         if self.gradient_as_bucket_view:
             b = self._bucketer
@@ -583,9 +602,42 @@ class DistributedDataParallel(nn.Module, Joinable):
         # walking the module tree every forward costs ~0.3 ms of host time a step
         bufs = getattr(self, "_modules_buffers", None)
         if bufs is None:
-            bufs = self._modules_buffers = [b for n, b in self.module.named_buffers()
-                                            if n not in self.parameters_to_ignore]
+            named = [(n, b) for n, b in self.module.named_buffers() if n not in self.parameters_to_ignore]
+            self._named_module_buffers = dict(named)
+            bufs = self._modules_buffers = [b for _, b in named]
         return bufs
+
+    @property
+    def named_module_buffers(self):
+        """{name: buffer} of the synchronised buffers (torch's attribute of the same
+        name, T:nn/parallel/distributed.py:1125-1133) — what a buffer comm hook gets."""
+        self._module_buffers()
+        return self._named_module_buffers
+
+    def _register_buffer_comm_hook(self, state, hook, comm_hook_location=None):
+        """torch's buffer comm hook (T:nn/parallel/distributed.py:1909-1951):
+        ``hook(state, named_module_buffers)`` replaces the rank-0 buffer broadcast,
+        before the forward (``_BufferCommHookLocation.PRE_FORWARD``) or after it
+        (``POST_FORWARD``, the default).  Futures it returns are awaited at the end
+        of the next backward, as the Reducer's ``_install_post_backward_futures``."""
+        if not callable(hook):
+            raise TypeError("buffer comm hook must be callable")
+        if comm_hook_location is None:
+            comm_hook_location = _BufferCommHookLocation.POST_FORWARD
+        # torch's own enum (torch.nn.parallel.distributed._BufferCommHookLocation) is accepted too
+        comm_hook_location = _BufferCommHookLocation[getattr(comm_hook_location, "name", comm_hook_location)]
+        self.buffer_hook = _BufferCommHook(hook, state, comm_hook_location)
+
+    def _run_buffer_hook(self):
+        bh = self.buffer_hook
+        futs = bh.buffer_comm_hook(bh.buffer_comm_hook_state, self.named_module_buffers)
+        if futs is not None:
+            self._post_bwd_futs = list(futs)
+
+    def _wait_post_backward_futures(self):
+        futs, self._post_bwd_futs = self._post_bwd_futs, []
+        for f in futs:
+            f.wait()
 
     def _broadcast_tensors(self, tensors, root: int = 0):
         """Broadcast tensors from group rank `root` (0 but under join): floating
@@ -643,6 +695,9 @@ class DistributedDataParallel(nn.Module, Joinable):
         one pack launch + one RCCL broadcast + one unpack launch per word size,
         plan cached across steps.  Integer buffers (BN num_batches_tracked,
         int64) travel as fp32 words — the kernels move them bit for bit."""
+        if self.buffer_hook is not None:
+            self._run_buffer_hook()  # the hook decides how buffers agree (torch: _sync_module_buffers)
+            return
         bufs = self._module_buffers()
         if self.world_size == 1 or not bufs:
             return
@@ -682,8 +737,8 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     # ------------------------------------------------------------------ forward
     def _will_sync_module_buffers(self):
-        return (self.world_size > 1 and self.require_forward_param_sync and self.broadcast_buffers
-                and len(self._module_buffers()) != 0)
+        return ((self.world_size > 1 or self.buffer_hook is not None) and self.require_forward_param_sync
+                and self.broadcast_buffers and len(self._module_buffers()) != 0)
 
     def forward(self, *inputs, **kwargs):
         L.flush_deferred()
@@ -703,7 +758,10 @@ class DistributedDataParallel(nn.Module, Joinable):
         elif self._div_factor != self.world_size and not self._join_config.enable:
             self._set_div_factor(float(self.world_size))
         joining = self._join_config.enable
-        if self._will_sync_module_buffers():
+        bh = self.buffer_hook
+        sync_bufs = self._will_sync_module_buffers()
+        post_fwd = bh is not None and bh.buffer_comm_hook_location == _BufferCommHookLocation.POST_FORWARD
+        if sync_bufs and not post_fwd:
             # under join rank 0 may have stopped: the highest still-training rank is the source
             self._sync_buffers(self._find_common_rank(self.rank, True) if joining else 0)
         if joining:
@@ -713,6 +771,8 @@ class DistributedDataParallel(nn.Module, Joinable):
             inputs = tuple(x.to(dev, non_blocking=True) if isinstance(x, torch.Tensor) else x for x in inputs)
             kwargs = {k: (v.to(dev, non_blocking=True) if isinstance(v, torch.Tensor) else v) for k, v in kwargs.items()}
         output = self.module(*inputs, **kwargs)
+        if sync_bufs and post_fwd:
+            self._sync_buffers()
         if grad_sync:
             self.require_forward_param_sync = True
             self._prepare_for_backward()
@@ -869,6 +929,8 @@ class DistributedDataParallel(nn.Module, Joinable):
                 if res is not None and res.data_ptr() != b.buffers[bi].data_ptr():
                     b.buffers[bi].copy_(res.reshape(-1)[: b.buffers[bi].numel()])
         self._pending = {}
+        if self._post_bwd_futs:
+            self._wait_post_backward_futures()
         L.check(L.lib().gs_bucketer_finalize(b.handle, self._stream), "gs_bucketer_finalize")
         if self._overlap is not None and not (b.flags & L.GS_BKT_AUTO_COLLECTIVE):
             # external collectives (gloo, host buckets): the grads exist once the

@@ -194,6 +194,40 @@ def test_ddp_rccl_max_ctas_ws1(cuda_device, rccl_pg):
     assert not ddp._own_comm and comm.handle is None
 
 
+def test_ddp_buffer_comm_hook_native_ws1(cuda_device, rccl_pg):
+    """A post-forward buffer comm hook on the C++-hook path: called once per
+    forward with the named buffers, its futures drained by the end of backward
+    (the native finalize), grads unchanged."""
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.manual_seed(0)
+    model = micro_resnet().to(cuda_device)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model)
+    seen = []
+
+    def hook(state, named):
+        seen.append(len(named))
+        fut = torch.futures.Future()
+        fut.set_result(None)
+        return [fut]
+
+    ddp._register_buffer_comm_hook(None, hook)
+    x = torch.rand(8, 3, 32, 32, device=cuda_device)
+    for it in range(3):
+        for p in params:
+            p.grad = None
+        ddp(x).sum().backward()
+        torch.cuda.synchronize()
+        assert ddp._native_on and ddp._post_bwd_futs == []
+        for i, p in enumerate(params):
+            assert torch.equal(p.grad, local[i]), f"iter {it} param {i}"
+    assert seen == [len(list(model.buffers()))] * 3
+
+
 def _ws2_worker(rank, ws, port, errq):
     try:
         import distributed_training_amd as D
