@@ -355,6 +355,13 @@ def _state_dict_keys(rank, ws):
     keys = list(d.state_dict().keys())
     assert keys[0] == "module.conv1.weight" and all(k.startswith("module.") for k in keys)
     assert len(keys) == len(m.state_dict())
+    # rccl_max_ctas only shapes a libgsync RCCL communicator: on CPU/gloo there is
+    # none to own, the DDP works as without it and close() leaves the group alone
+    c = D.DistributedDataParallel(_micro(), rccl_max_ctas=8)
+    assert c._comm is None and not c._own_comm
+    assert c._get_ddp_logging_data()["rccl_max_ctas"] is None
+    c(torch.rand(2, 3, 32, 32)).sum().backward()
+    c.close()
 
 
 def test_state_dict_has_module_prefix():
