@@ -314,8 +314,12 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     for name, kw in variants:
         kw = dict(kw)
         bdt = kw.pop("bucket_dtype", bucket_dtype)
-        v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bdt,
-                                      gradient_as_bucket_view=args.grad_as_bucket_view, **kw)
+        try:
+            v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bdt,
+                                          gradient_as_bucket_view=args.grad_as_bucket_view, **kw)
+        except Exception as e:  # e.g. RCCL refusing a communicator config: every rank alike
+            rows[name] = {"error": f"{type(e).__name__}: {e}"[:300], "parity": None}
+            continue
 
         def fwd_bwd():
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -366,10 +370,12 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
         v.close()
     base = (rows["torch"]["images_per_sec"] + rows["torch_again"]["images_per_sec"]) / 2
     best, best_ips = "torch", base * (1 + POLICY_MARGIN)
-    if "bf16_buckets" in rows:
+    if "images_per_sec" in rows.get("bf16_buckets", {}):
         rows["bf16_buckets"]["vs_torch"] = rows["bf16_buckets"]["images_per_sec"] / base
     for name in ("xgmi", "last_bucket_cap_1MiB", "rccl_cta_cap_16"):
         r = rows[name]
+        if "error" in r:
+            continue
         r["vs_torch"] = r["images_per_sec"] / base
         if r["parity"] and r["parity"].get("ok") and r["images_per_sec"] >= best_ips:
             best, best_ips = name, r["images_per_sec"]
