@@ -368,6 +368,48 @@ def test_state_dict_has_module_prefix():
     _run(_state_dict_keys, 1)
 
 
+def _zero_sized(rank, ws):
+    """A zero-element parameter (used in the forward) rides in a bucket as an
+    empty slot: grads equal torch's DDP bit for bit, fused SGD equals torch's."""
+    import distributed_training_amd as D
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.l = nn.Linear(6, 5)
+            self.z = nn.Parameter(torch.empty(0))
+            self.l2 = nn.Linear(5, 3)
+
+        def forward(self, x):
+            return self.l2(torch.relu(self.l(x) + self.z.sum()))
+
+    torch.manual_seed(0)
+    m1, m2 = M(), M()
+    m2.load_state_dict(m1.state_dict())
+    a, b = D.DistributedDataParallel(m1), TDDP(m2)
+    oa = D.FusedSGD(a.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ob = torch.optim.SGD(b.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=False)
+    g = torch.Generator().manual_seed(40 + rank)
+    for it in range(3):
+        x = torch.rand(4, 6, generator=g)
+        for mod in (a, b):
+            mod(x).square().sum().backward()
+        for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+            assert (p.grad is None) == (q.grad is None) and (p.grad is None or torch.equal(p.grad, q.grad)), \
+                f"it {it} {n}"
+        oa.step()
+        ob.step()
+        oa.zero_grad()
+        ob.zero_grad()
+        for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7, msg=f"it {it} {n}")
+
+
+def test_zero_sized_parameter_matches_torch():
+    _run(_zero_sized, 2)
+
+
 def _frozen(rank, ws):
     """A frozen layer (requires_grad=False): torch's DDP leaves it out of the
     buckets but still broadcasts it from rank 0 at wrap time; grads of the

@@ -194,6 +194,50 @@ def test_ddp_rccl_max_ctas_ws1(cuda_device, rccl_pg):
     assert not ddp._own_comm and comm.handle is None
 
 
+def test_ddp_zero_sized_parameter_ws1(cuda_device, rccl_pg):
+    """A zero-element parameter in the model (an empty bucket slot, a NULL grad
+    pointer) on the C++-hook RCCL path: every grad equals the local grad and the
+    fused SGD step equals the oracle."""
+    from distributed_training_amd import DistributedDataParallel, FusedSGD
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.l = torch.nn.Linear(64, 32)
+            self.z = torch.nn.Parameter(torch.empty(0))
+            self.l2 = torch.nn.Linear(32, 8)
+
+        def forward(self, x):
+            return self.l2(torch.relu(self.l(x) + self.z.sum()))
+
+    torch.manual_seed(0)
+    model = M().to(cuda_device)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model)
+    opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    bufs = {}
+    for it in range(3):
+        x = torch.rand(16, 64, device=cuda_device)
+        ddp(x).square().sum().backward()
+        torch.cuda.synchronize()
+        assert ddp._native_on
+        for i, p in enumerate(params):
+            assert torch.equal(p.grad, local[i]), f"iter {it} param {i}"
+        ref = []
+        for i, p in enumerate(params):
+            b = bufs.get(i)
+            ref.append(O.sgd(to_np(p).reshape(-1), to_np(p.grad).reshape(-1), b, 0.1, 0.9, 0.0, 1e-4,
+                             False, False, b is None))
+        opt.step()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            assert np.array_equal(to_np(p).reshape(-1), ref[i][0]), f"iter {it} param {i} weights"
+            bufs[i] = ref[i][1]
+        opt.zero_grad()
+
+
 def test_ddp_buffer_comm_hook_native_ws1(cuda_device, rccl_pg):
     """A post-forward buffer comm hook on the C++-hook path: called once per
     forward with the named buffers, its futures drained by the end of backward
