@@ -410,6 +410,46 @@ def test_zero_sized_parameter_matches_torch():
     _run(_zero_sized, 2)
 
 
+def _tied(rank, ws):
+    """A weight shared by two layers (one parameter, two uses): one bucket slot,
+    its grad the sum of both uses, averaged once — as torch's DDP, which keeps
+    the parameter once (T:nn/parallel/distributed.py _build_params_for_reducer
+    dedups by identity)."""
+    import distributed_training_amd as D
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(6, 6)
+            self.b = nn.Linear(6, 6)
+            self.b.weight = self.a.weight
+            self.c = nn.Linear(6, 2)
+
+        def forward(self, x):
+            return self.c(self.b(torch.tanh(self.a(x))))
+
+    torch.manual_seed(0)
+    m1, m2 = M(), M()
+    m2.load_state_dict(m1.state_dict())
+    a, b = D.DistributedDataParallel(m1), TDDP(m2)
+    assert len(a._params) == len(list(m1.parameters())) == 5
+    g = torch.Generator().manual_seed(60 + rank)
+    for it in range(3):
+        x = torch.rand(4, 6, generator=g)
+        for mod in (a, b):
+            mod(x).square().sum().backward()
+        for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+            assert torch.equal(p.grad, q.grad), f"it {it} {n}"
+        m1.zero_grad()
+        m2.zero_grad()
+    assert m1.a.weight is m1.b.weight
+
+
+def test_tied_weights_match_torch():
+    _run(_tied, 2)
+
+
 def _frozen(rank, ws):
     """A frozen layer (requires_grad=False): torch's DDP leaves it out of the
     buckets but still broadcasts it from rank 0 at wrap time; grads of the
