@@ -450,6 +450,44 @@ def test_tied_weights_match_torch():
     _run(_tied, 2)
 
 
+def _eval_interleaved(rank, ws):
+    """Validation forwards between training steps (model.eval() under no_grad,
+    then back to train()): outputs, BN buffers and grads equal torch's DDP at
+    every step — including torch's rule that a forward after a no-grad forward
+    skips the buffer broadcast (require_forward_param_sync)."""
+    import distributed_training_amd as D
+    from torch.nn.parallel import DistributedDataParallel as TDDP
+
+    torch.manual_seed(2)
+    m1, m2 = _micro(), _micro()
+    m2.load_state_dict(m1.state_dict())
+    a, b = D.DistributedDataParallel(m1), TDDP(m2)
+    g = torch.Generator().manual_seed(80 + rank)
+    for it in range(4):
+        x = torch.rand(3, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (3,), generator=g)
+        xv = torch.rand(2, 3, 32, 32, generator=g)
+        for mod in (a, b):
+            mod.train()
+            nn.functional.cross_entropy(mod(x), y).backward()
+        for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+            assert torch.equal(p.grad, q.grad), f"it {it} {n}"
+        outs = []
+        for mod in (a, b):
+            mod.eval()
+            with torch.no_grad():
+                outs.append(mod(xv))
+        assert torch.equal(outs[0], outs[1]), f"it {it} eval output"
+        for (n, x1), x2 in zip(m1.named_buffers(), m2.buffers()):
+            assert torch.equal(x1, x2), f"it {it} {n}"
+        m1.zero_grad()
+        m2.zero_grad()
+
+
+def test_eval_forwards_between_steps_match_torch():
+    _run(_eval_interleaved, 2)
+
+
 def _frozen(rank, ws):
     """A frozen layer (requires_grad=False): torch's DDP leaves it out of the
     buckets but still broadcasts it from rank 0 at wrap time; grads of the
