@@ -1,7 +1,8 @@
 """Runs only one libgsync grad-sync kernel over a model's parameter set, N
 launches — the unit a rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE) measures.
     python scripts/kernel_only.py <model> <launches> <op> [replicas]
-op: sgd | adam (update plan, as FusedSGD / FusedAdam build it),
+op: sgd | adam (update plan, as FusedSGD / FusedAdam build it), clipsgd (the folded clip
+    path on the update plan: gs_sqnorm_partial + the clipped SGD, max_norm 1.0),
     pack | pack16 | unpack | unpacksq | sqnorm | sqpart (bucket-layout plan, align 64;
     sqpart = gs_sqnorm_partial, the folded clip's Σg² launch)."""
 import os
@@ -21,7 +22,7 @@ dev = torch.device("cuda", 0)
 shapes = [p.shape for p in MODELS[model]().parameters()] * reps
 n = [torch.Size(s).numel() for s in shapes]
 gs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
-if op in ("sgd", "adam"):
+if op in ("sgd", "adam", "clipsgd"):
     ps = [torch.randn(s, device=dev) for s in shapes]
     bs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
     vs = [torch.rand(s, device=dev) * 1e-4 for s in shapes] if op == "adam" else None
@@ -37,6 +38,10 @@ for _ in range(iters):
     if op == "adam":
         plan.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5)
     elif op == "sgd":
+        plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)
+    elif op == "clipsgd":
+        plan.sqnorm_partial(1, torch.float32)
+        plan.set_clip(1.0)
         plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)
     elif op in ("pack", "pack16"):
         plan.pack(1, torch.float32, flat, 0.125, 1)

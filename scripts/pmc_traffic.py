@@ -11,7 +11,8 @@ import sys
 
 
 KERNEL = {"sgd": "SgdOp", "adam": "AdamOp", "pack": "PackOp", "pack16": "PackOp", "unpack": "UnpackOp",
-          "unpacksq": "UnpackOp", "sqnorm": "SqnormOp"}
+          "unpacksq": "UnpackOp", "sqnorm": "SqnormOp", "sqpart": "SqnormOp",
+          "clipsgd": "SgdOp"}  # clipsgd: the clipped update's own dispatches (its Σg² launch is sqpart)
 
 
 def load(d, counter, tag="SgdOp"):
