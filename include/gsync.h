@@ -96,8 +96,9 @@ int gs_comm_get_unique_id(uint8_t* out /* [gs_comm_unique_id_bytes()] */);
 int gs_comm_create(int rank, int world, const uint8_t* uid, int device, gs_comm** out);
 /* The same with RCCL's per-collective workgroup (CTA) cap (ncclConfig_t
  * maxCTAs; <= 0: RCCL's default): fewer CUs taken from the backward kernels the
- * in-step collectives overlap.  No torch counterpart (ProcessGroupNCCL's
- * Options::config, T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp). */
+ * in-step collectives overlap.  Replaces ProcessGroupNCCL's Options::config
+ * (an ncclConfig_t handed to ncclCommInitRankConfig,
+ * T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp:531). */
 int gs_comm_create_ex(int rank, int world, const uint8_t* uid, int device, int max_ctas, gs_comm** out);
 int gs_comm_destroy(gs_comm* c);
 /* ncclCommAbort: for the failure path (timeout / peer death) */
