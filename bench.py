@@ -27,8 +27,10 @@ import socket
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+T_START = time.time()  # --wall-budget-s counts from here (covers warm-up's MIOpen compiles)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -36,6 +38,31 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
 HBM_COPY_GBPS = 6290.0  # MI355X_MICROARCH.md's measured float4 copy ceiling (report both)
 XGMI_LINK_GBPS = 153.0  # per point-to-point link; bus roofline (n-1) x 153
+
+
+def _host_cores() -> dict:
+    """The host cores this process may use: its CPU affinity, capped by the
+    cgroup's CPU quota when one is set (a GPU box's share of a larger machine —
+    os.cpu_count() reports the whole machine there)."""
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = int(parts[0]) / int(f.read().split()[0])
+            if quota is not None:
+                break
+        except (OSError, ValueError, IndexError, ZeroDivisionError):
+            continue
+    used = max(1, min(affinity, int(quota)) if quota else affinity)
+    return {"cores_used": used, "affinity": affinity, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "rule": "min(CPU affinity, cgroup CPU quota); the torch DDP/gloo ranks split them, cores // ws each"}
 
 
 def _free_port():
@@ -88,10 +115,11 @@ def parse():
                     help="after the headline: BASELINE configs[4] (Colossal shim, ResNet-152 fp32 grads, fp16 "
                          "autocast, HybridAdam, 128 img/GPU) on the same ranks, the line's `colossal` object "
                          "(-1: at N > 1 on the DDP engine)")
-    ap.add_argument("--leg-budget-s", type=float, default=360.0,
-                    help="N > 1: if the optional legs after the timed region (standalone collectives, parity, "
-                         "policy A/B) overrun this, print the line with the legs done so far and end every rank "
-                         "(0 = no watchdog)")
+    ap.add_argument("--wall-budget-s", type=float, default=540.0,
+                    help="whole-run wall budget from process start (warm-up compiles included): an optional leg "
+                         "after the timed region runs only if its cost estimate (LEG_COST_S, measured) fits what "
+                         "is left, else it is recorded as skipped; a leg still running past the budget ends "
+                         "every rank after the line is printed, exit status 3 (0 = no budget)")
     ap.add_argument("--parity", type=int, default=1,
                     help="after the timed region: one self-checked step (distributed_training_amd.parity)")
     ap.add_argument("--kernel-rates", type=int, default=1,
@@ -169,21 +197,19 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
             "timing": "HIP events on libgsync's comm stream, median of 10 after 3 warmup, ops back to back"}
 
 
-def grad_sync_kernel_rates(params, dev, iters=20):
-    """Every grad-sync kernel of the step on this model's parameter set, warm
-    and alone on the GPU (after the timed region): pack fp32 x1/ws, pack to
-    bf16, unpack (+ fused Σg²), Σg² on a bucket-layout plan (64-element
-    alignment, as the DDP buckets), the update kernels on an update plan (as
-    FusedSGD / FusedAdam build it).  Algorithmic bytes / average kernel time
-    (plan launch timer: HIP events on the launch stream around each kernel)
-    against the 8 TB/s HBM peak — the north star's ">= 70 % of HBM peak"
-    covers all of them, not just the headline update kernel."""
+def _kernel_rows(shapes, dev, iters):
+    """Every grad-sync kernel of the step on one parameter set (shapes), warm and
+    alone on the GPU: pack fp32 x1/ws, pack to bf16, unpack (+ fused Σg²), Σg² on
+    a bucket-layout plan (64-element alignment, as the DDP buckets), the update
+    kernels on an update plan (as FusedSGD / FusedAdam build it).  Algorithmic
+    bytes / average per call (plan launch timer: HIP events on the launch stream
+    around each kernel, every launch of a multi-launch call counted)."""
     from distributed_training_amd.multi_tensor import TensorListPlan, update_task_units
 
-    numels = [p.numel() for p in params]
+    numels = [int(torch.Size(s).numel()) for s in shapes]
     n = sum(numels)
     g = torch.Generator(device=dev).manual_seed(7)
-    grads = [torch.randn(p.shape, device=dev, generator=g) * 0.01 for p in params]
+    grads = [torch.randn(s, device=dev, generator=g) * 0.01 for s in shapes]
     plan = TensorListPlan(numels, dev, align=64)
     plan.set_ptrs(1, grads)
     flat = torch.zeros(plan.flat_numel, device=dev)
@@ -209,10 +235,11 @@ def grad_sync_kernel_rates(params, dev, iters=20):
             ("sqnorm_f32", 4 * n, lambda: plan.sqnorm(1, torch.float32, sq))):
         ms = rate(fn, plan)
         rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9}
+    del flat, flat16
     up = TensorListPlan(numels, dev, task_units=update_task_units(dev))
-    ps = [torch.randn(p.shape, device=dev, generator=g) for p in params]
-    bs = [torch.randn(p.shape, device=dev, generator=g) * 0.01 for p in params]
-    vs = [torch.rand(p.shape, device=dev, generator=g) * 1e-4 for p in params]
+    ps = [torch.randn(s, device=dev, generator=g) for s in shapes]
+    bs = [torch.randn(s, device=dev, generator=g) * 0.01 for s in shapes]
+    vs = [torch.rand(s, device=dev, generator=g) * 1e-4 for s in shapes]
     up.set_ptrs(0, ps)
     up.set_ptrs(1, grads)
     up.set_ptrs(2, bs)
@@ -239,11 +266,128 @@ def grad_sync_kernel_rates(params, dev, iters=20):
     rows["adam"] = {"alg_bytes": 28 * n, "avg_ms": ms, "GBps": 28 * n / (ms * 1e-3) / 1e9}
     for r in rows.values():
         r["frac"] = r["GBps"] / HBM_PEAK_GBPS
-    return {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS,
-            "timing": "after the timed region, warm, alone on the GPU; plan launch timer (HIP events on the "
-                      f"launch stream around each kernel), average of {iters} calls (kernel-trace durations: "
-                      "profiles/r3/r3i_trace_rates.json)",
-            "min_frac": min(r["frac"] for r in rows.values())}
+    return n, rows
+
+
+def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
+    """configs[3]'s end-of-step clip path as its N>1 branch runs it (zero.py), on
+    one rank's shard of an N=`shard_world` ZeRO-2 run (ResNet-50: 25.56 M / 8 ≈
+    3.2 M elements; bf16 grads, fp32 master / exp_avg / exp_avg_sq, bf16 param
+    write), every launch and the collective timed together (HIP events on the
+    stream they run on), over the engine's RCCL communicator (one rank here):
+
+    * ``clip_path_zero_n8``: Σg² group sums of the shard (gs_sqnorm_partial_out)
+      -> ONE SUM all-reduce of those <= 64 floats -> the AdamW update folding them
+      (gs_plan_set_clip_groups) — round 4's path;
+    * ``clip_path_zero_n8_scalar``: round 3's form — Σg² with its in-kernel
+      combine -> SUM all-reduce of the scalar -> the update (gs_plan_set_clip).
+
+    Algorithmic bytes per element: Σg² 2 (bf16 read) + AdamW 28 (p r/w 8, g 2,
+    m r/w 8, v r/w 8, bf16 param 2) = 30."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.multi_tensor import TensorListPlan, update_task_units
+
+    q = shard_world * 64
+    shard = (n_params + q - 1) // q * q // shard_world
+    g = torch.Generator(device=dev).manual_seed(11)
+    master = torch.randn(shard, device=dev, generator=g)
+    grads = (torch.randn(shard, device=dev, generator=g) * 1e-3).to(torch.bfloat16)
+    m = torch.randn(shard, device=dev, generator=g) * 1e-3
+    v = torch.rand(shard, device=dev, generator=g) * 1e-6
+    p16 = master.to(torch.bfloat16)
+    plan = TensorListPlan([shard], dev, task_units=update_task_units(dev))
+    for k, t in enumerate((master, grads, m, v, p16)):
+        plan.set_ptrs(k, [t])
+    groups = torch.zeros(L.GS_RED_GROUPS, device=dev)
+    sq = torch.zeros(1, device=dev)
+    out = torch.zeros(3, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def adam():
+        plan.adam(torch.bfloat16, 1e-3, 0.8, 0.999, 1e-8, 3e-7, True, False, -1e-3, 0.5, lowp_dtype=torch.bfloat16)
+
+    def folded():
+        n = plan.sqnorm_partial_out(1, torch.bfloat16, groups)
+        comm.all_reduce(groups[:n], stream=stream)
+        plan.set_clip_groups(1.0, 1e-6, groups, n, out=out)
+        adam()
+
+    def scalar():
+        plan.sqnorm(1, torch.bfloat16, sq)
+        comm.all_reduce(sq, stream=stream)
+        plan.set_clip(1.0, 1e-6, sq, out=out)
+        adam()
+
+    rows = {}
+    for name, fn in (("clip_path_zero_n8", folded), ("clip_path_zero_n8_scalar", scalar)):
+        for _ in range(3):
+            fn()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+        plan.timer_enable(4 * iters)
+        for a, b in evs:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        kern = plan.timer_read()
+        plan.timer_enable(0)
+        ms = sum(a.elapsed_time(b) for a, b in evs) / iters
+        nbytes = 30 * shard
+        rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9,
+                      "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "shard_elems": shard,
+                      "kernels_ms": sum(kern) / iters,
+                      "launches": ("sqnorm_partial_out + all_reduce(<=64 floats) + clipped AdamW"
+                                   if name == "clip_path_zero_n8" else
+                                   "sqnorm (in-kernel combine) + all_reduce(scalar) + clipped AdamW")}
+    plan.set_clip(None)
+    rows["clip_path_zero_n8"]["vs_scalar_form"] = (rows["clip_path_zero_n8_scalar"]["avg_ms"]
+                                                   / rows["clip_path_zero_n8"]["avg_ms"])
+    return rows
+
+
+def _beyond_ic_shapes():
+    """ResNet-152's parameter shapes twice: 120.4 M elements, a 481 MB gradient —
+    every kernel's working set is well past the 256 MiB Infinity Cache."""
+    from distributed_training_amd.resnet import MODELS
+
+    with torch.device("meta"):
+        m = MODELS["resnet152"](num_classes=1000)
+    return [tuple(p.shape) for p in m.parameters()] * 2
+
+
+def _beyond_ic_roofline(kernel_rates, zero, args):
+    """The headline update kernel's true-HBM rate, measured in this run: the same
+    kernel on the >256 MiB working set of grad_sync_kernel_rates (the in-step
+    `frac` runs on ResNet-50's 511 MB read/write set, partly served by the 256 MiB
+    Infinity Cache right after the unpack wrote the grads)."""
+    if not kernel_rates or zero is not None or args.engine != "ddp" or "beyond_ic" not in kernel_rates:
+        return {}
+    row = kernel_rates["beyond_ic"]["kernels"]["sgd_momentum_wd" if args.optimizer == "sgd" else "adam"]
+    return {"frac_beyond_ic": row["frac"], "beyond_ic": {
+        "achieved": row["GBps"], "avg_launch_ms": row["avg_ms"], "algorithmic_bytes_per_launch": row["alg_bytes"],
+        "set": kernel_rates["beyond_ic"]["set"], "timing": "plan launch timer, grad_sync_kernels.beyond_ic"}}
+
+
+def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
+    """Every grad-sync kernel of the step, after the timed region, warm and alone
+    on the GPU, on this model's parameter set (``kernels``) and on a >256 MiB
+    working set (``kernels_beyond_ic``: ResNet-152 x 2, true-HBM rates — SURVEY
+    §8(d)), against the 8 TB/s HBM peak: the north star's ">= 70 % of HBM peak"
+    covers all of them, not just the headline update kernel.  With the engine's
+    one-rank RCCL communicator: configs[3]'s N>1 clip path at its N=8 shard."""
+    n, rows = _kernel_rows([tuple(p.shape) for p in params], dev, iters)
+    n_big, big = _kernel_rows(_beyond_ic_shapes(), dev, iters)
+    torch.cuda.empty_cache()
+    out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS,
+           "timing": "after the timed region, warm, alone on the GPU; plan launch timer (HIP events on the "
+                     f"launch stream around each kernel), average of {iters} calls (kernel-trace durations: "
+                     "profiles/r3/r3i_trace_rates.json)",
+           "min_frac": min(r["frac"] for r in rows.values()),
+           "beyond_ic": {"params": n_big, "set": "ResNet-152 parameter shapes x 2 (> 256 MiB Infinity Cache)",
+                         "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}
+    if comm is not None and world == 1:
+        out.update(zero_clip_path_rows(n, dev, comm, iters=iters))
+    return out
 
 
 class _BenchColl:
@@ -282,6 +426,18 @@ def _engine_comm(ddp, zero):
         if c is not None:
             return c
     return None
+
+
+# Cost estimates of the optional legs after the timed region (seconds), for the
+# --wall-budget-s skip decision: the larger of the N=1 run with every leg forced on
+# (profiles/r3/r3n_bench_n1_all_legs.json leg_seconds) and the 4-rank full-size
+# rehearsal (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json), doubled,
+# and at least 5 s; zero2 / colossal include their first-step MIOpen compiles.
+LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
+              "zero2": 2 * 8.4, "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 16.2}
+# the reference's DeepSpeed optimizer (R:resnet/deepspeed/deepspeed_train.py:175-186): "Adam" in
+# AdamW mode, betas (0.8, 0.999), eps 1e-8, weight_decay 3e-7; gradient_clipping 1.0 (:195)
+DS_ADAM = dict(lr=1e-3, betas=(0.8, 0.999), eps=1e-8, weight_decay=3e-7)
 
 
 # DESIGN §8 decision rule for the bucket policy (row N1), fixed before the
@@ -403,8 +559,8 @@ def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
 
     torch.manual_seed(0)
     model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
-    zero = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=1e-3, momentum=0.9, weight_decay=3e-7,
-                            reduce_bucket_size=int(5e7), gradient_clipping=1.0)
+    zero = ZeroDataParallel(model, stage=2, optimizer="adamw", momentum=0.9, reduce_bucket_size=int(5e7),
+                            gradient_clipping=1.0, **DS_ADAM)
     g = torch.Generator(device=dev).manual_seed(4321 + rank)
     x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
     x = x.to(torch.bfloat16)
@@ -436,6 +592,7 @@ def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
     upd_ms = sum(upd) / len(upd) if upd else None
     out = {"engine": "zero2", "config": "BASELINE configs[3]: ResNet-50 bf16 model, ZeRO-2 reduce-scatter + "
                                         "AdamW on fp32 master shards + all-gather, clip 1.0",
+           "optimizer": dict(DS_ADAM, kind="adamw", gradient_clipping=1.0),
            "images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3,
            "per_gpu_batch": args.batch, "steps": steps, "warmup": warmup,
            "shard_update": {"avg_launch_ms": upd_ms, "alg_bytes_per_launch": 28 * shard,
@@ -592,7 +749,7 @@ def main():
         bf = torch.bfloat16
         ddp = FSDP(model, sharding_strategy=ShardingStrategy.SHARD_GRAD_OP, device_id=dev,
                    mixed_precision=MixedPrecision(param_dtype=bf, reduce_dtype=bf, buffer_dtype=bf))
-        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3, weight_decay=3e-7, fused=True)
+        opt = torch.optim.AdamW(ddp.parameters(), fused=True, **DS_ADAM)
         bytes_per_param = 28
         grad_bytes = n_params * 2
     elif args.impl == "torch":
@@ -656,8 +813,7 @@ def main():
         model = model.to(torch.bfloat16)
         zero = ZeroDataParallel(model, stage=2 if args.engine == "zero2" else 1,
                                 optimizer="sgd" if args.optimizer == "sgd" else "adamw",
-                                lr=1e-3, momentum=0.9, weight_decay=3e-7, reduce_bucket_size=int(5e7),
-                                gradient_clipping=1.0)
+                                momentum=0.9, reduce_bucket_size=int(5e7), gradient_clipping=1.0, **DS_ADAM)
         ddp = model
         # per shard param: p r/w fp32, g r bf16, states r/w fp32, bf16 param write
         bytes_per_param = (4 + 4 + 2 + 8 + 2) if args.optimizer == "sgd" else (4 + 4 + 2 + 16 + 2)
@@ -948,6 +1104,7 @@ def main():
                 "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
                 **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
                 **({"rocprof": trace_check} if trace_check else {}),
+                **_beyond_ic_roofline(kernel_rates, zero, args),
             },
             "grad_sync": grad_sync,
             "grad_sync_kernels": kernel_rates,
@@ -969,23 +1126,45 @@ def main():
         return line
 
     # ---- after the timed region.  The headline is complete here; what follows are
-    # optional legs (tail split, standalone collectives, kernel rates, the parity
-    # step, the bucket-policy A/B).  Each leg that raises is recorded in
-    # "leg_errors" instead of losing the line; at N > 1 a watchdog prints the line
-    # with the legs completed so far and ends every rank if the legs overrun
-    # --leg-budget-s (a collective that never completes would otherwise cost the
-    # headline too).
+    # optional legs, in order of evidence value: the tail split, the self-checked
+    # parity step, the standalone collectives (bus bandwidth), the kernel rates, the
+    # ZeRO-2 leg (configs[3]), the Colossal leg (configs[4]), the bucket-policy A/B.
+    # --wall-budget-s (from process start) gates each: a leg whose LEG_COST_S estimate
+    # does not fit what is left is skipped and named in "leg_errors" (the decision uses
+    # the MAX of the ranks' clocks, so every rank skips alike); a leg that raises is
+    # recorded there too instead of losing the line; a leg still running when the
+    # budget ends (a hung collective) gets a watchdog that prints the line with the
+    # legs completed so far and ends every rank with exit status 3.
     tail = timeline = tail_timed = None
     coll = kernel_rates = parity = policy_ab = zero2 = colossal = None
     leg_errors: dict = {}
     current_leg = ["start"]
 
     leg_seconds: dict = {}
+    budget = args.wall_budget_s
+
+    def fits(name):
+        if budget <= 0:
+            return True
+        left = budget - coll_h.max(time.time() - T_START)
+        if LEG_COST_S.get(name, 5.0) <= left:
+            return True
+        leg_errors[name] = (f"skipped: estimated {LEG_COST_S.get(name, 5.0):.0f} s > {max(left, 0.0):.0f} s left "
+                            f"of --wall-budget-s {budget:.0f}")
+        if rank == 0:
+            print(f"[bench] leg {name} {leg_errors[name]}", file=sys.stderr, flush=True)
+        return False
+
+    hang_leg = os.environ.get("GSYNC_BENCH_TEST_HANG_LEG")  # test hook: this leg never returns
 
     def leg(name, fn):
+        if name != hang_leg and not fits(name):
+            return None
         current_leg[0] = name
         t_leg = time.perf_counter()
         try:
+            while name == hang_leg:  # tests/test_gpu_zz_bench.py: the watchdog's exit path
+                time.sleep(5)
             return fn()
         except Exception as ex:  # recorded, the line still prints
             import traceback
@@ -997,7 +1176,7 @@ def main():
             leg_seconds[name] = round(time.perf_counter() - t_leg, 2)
 
     watchdog = None
-    if world > 1 and args.leg_budget_s > 0:
+    if budget > 0:
         import threading
 
         def expire():
@@ -1012,13 +1191,15 @@ def main():
                           "config": {"workload": f"{args.model} synthetic 224x224 training, {args.batch} img/GPU",
                                      "parallelism": f"dp{world}", "global_batch": args.batch * world},
                           "line_error": repr(ex)}
-                ln["legs_incomplete"] = {"leg": current_leg[0], "budget_s": args.leg_budget_s}
+                ln["legs_incomplete"] = {"leg": current_leg[0], "wall_budget_s": budget}
                 print(json.dumps(ln), flush=True)
-            print(f"[bench] rank {rank}: legs overran {args.leg_budget_s}s in {current_leg[0]}: exiting",
-                  file=sys.stderr, flush=True)
-            os._exit(0)
+            print(f"[bench] rank {rank}: leg {current_leg[0]} still running at the {budget:.0f} s wall budget: "
+                  "exiting with status 3", file=sys.stderr, flush=True)
+            os._exit(3)
 
-        watchdog = threading.Timer(args.leg_budget_s, expire)
+        # a leg only starts when its estimate fits the budget: one that is still running
+        # 30 s past it overran its estimate several times over (a hang), not a slow box
+        watchdog = threading.Timer(max(1.0, T_START + budget + 30.0 - time.time()), expire)
         watchdog.daemon = True
         watchdog.start()
 
@@ -1040,13 +1221,7 @@ def main():
             ddp.set_timeline(1)
             opt.kernel_ms()  # drop the untimed steps' launches
 
-
     leg("tail_split", tail_leg)
-    if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
-        coll = leg("collective_bench", lambda: collective_bench(ddp, zero, world))
-    if args.impl == "libgsync" and args.kernel_rates and rank == 0:
-        kernel_rates = leg("kernel_rates", lambda: grad_sync_kernel_rates(
-            [p for p in model.parameters() if p.requires_grad] if zero is None else zero.params, dev))
 
     if args.parity and args.impl == "libgsync" and not args.graph:
         from distributed_training_amd import parity as PC
@@ -1071,13 +1246,14 @@ def main():
         if rank == 0:
             print(f"[bench] parity: {json.dumps(parity)}", file=sys.stderr, flush=True)
 
-    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
-    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
-            and not args.optimizer_overlap):
-        # after every reading of the headline DDP above: it is closed here
-        policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
-        if rank == 0 and policy_ab is not None:
-            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
+    if args.impl == "libgsync" and (args.collective_bench == 1 or (args.collective_bench == -1 and world > 1)):
+        coll = leg("collective_bench", lambda: collective_bench(ddp, zero, world))
+    if args.impl == "libgsync" and args.kernel_rates:
+        # rank 0 measures; the others wait in the next leg's (or the end's) collective
+        kernel_rates = leg("kernel_rates", lambda: grad_sync_kernel_rates(
+            [p for p in model.parameters() if p.requires_grad] if zero is None else zero.params, dev,
+            comm=_engine_comm(ddp, zero), world=world) if rank == 0 else None)
+
     want_zero = args.zero_leg == 1 or (args.zero_leg == -1 and world > 1)
     if want_zero and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
         zero2 = leg("zero2", lambda: zero2_leg(args, world, rank, dev, coll_h))
@@ -1091,6 +1267,13 @@ def main():
         if rank == 0 and colossal is not None:
             print(f"[bench] colossal leg: {colossal['images_per_sec']:.1f} images/s, "
                   f"parity {colossal['parity'].get('ok')}", file=sys.stderr, flush=True)
+    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
+    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
+            and not args.optimizer_overlap):
+        # after every reading of the headline DDP above: it is closed here
+        policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
+        if rank == 0 and policy_ab is not None:
+            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
     current_leg[0] = "done"
     if watchdog is not None:
         watchdog.cancel()
@@ -1103,7 +1286,8 @@ def main():
     if args.cpu_baseline and world == 1:
         from oracle.cpu_ddp_baseline import cpu_model_name, run as cpu_run
 
-        cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        hc = _host_cores()
+        cores = hc["cores_used"]
         # leg 1 (the headline unit): the reference's torch-DDP/gloo path on this workload's model at 224x224;
         # leg 2: BASELINE configs[0], the reference's own workload (ResNet-18 CIFAR, 100 img/rank, ws=2)
         cb = cpu_run(model=args.model, batch=16, ws=2, cores=cores, steps=5, warmup=1, port=_free_port())
@@ -1112,6 +1296,7 @@ def main():
             "value": cb["images_per_sec"],
             "unit": "images/sec",
             "cores": cb["cores"],
+            "cores_available": hc,
             "cpu_model": cpu_model_name(),
             "kind": "port",
             "gloo_allreduce_busbw_GBps": cb["gloo_allreduce_busbw_GBps"],

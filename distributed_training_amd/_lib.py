@@ -31,6 +31,7 @@ GS_DEV_HOST, GS_DEV_HIP = 0, 1
 GS_SUM, GS_PROD, GS_MAX, GS_MIN, GS_AVG = 0, 1, 2, 3, 4
 GS_SCALE_NONE, GS_SCALE_MUL, GS_SCALE_DIV = 0, 1, 2
 GS_PLAN_SLOTS = 5
+GS_RED_GROUPS = 64  # gs_sqnorm_partial_out: at most this many group sums
 GS_BKT_AUTO_COLLECTIVE = 1
 GS_BKT_GRAD_VIEW = 2
 GS_BKT_NO_SCALE = 4
@@ -99,6 +100,8 @@ SIGNATURES = {
     "gs_sum": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_sqnorm_partial": (_c_int, [_vp, _c_int, _c_int, _vp]),
     "gs_plan_set_clip": (_c_int, [_vp, _vp, _c_f, _c_f, _c_f, _c_f, _vp]),
+    "gs_sqnorm_partial_out": (_c_int, [_vp, _c_int, _c_int, _vp, _p_i32, _vp]),
+    "gs_plan_set_clip_groups": (_c_int, [_vp, _vp, ctypes.c_int32, _c_f, _c_f, _c_f, _c_f, _vp]),
     "gs_rng_state_bytes": (_c_int, []),
     "gs_rng_draw_u32": (_c_int, [_vp, _c_i64, _c_i64, _vp]),
     "gs_randperm": (_c_int, [ctypes.c_uint64, _c_i64, _vp]),

@@ -81,6 +81,10 @@ constexpr int kBlock = 256;         // 4 waves of 64
 // r1r_grid_sweep.jsonl); GS_MAX_GRID=2048 restores the one-resident-wave cap
 constexpr int kMaxGrid = 65536;
 constexpr int kGridLimit = 65536;   // hard cap (partials buffer); GS_MAX_GRID env for tuning
+// fused reductions: at most kRedMaxGroups group sums (one per lane of the
+// folding wave), each counter / group sum on its own 128-B line
+constexpr int kRedMaxGroups = GS_RED_GROUPS;
+constexpr int kRedSyncStride = 32;
 
 struct Seg {
   int64_t unit_begin;  // first unit inside the tensor (interleaved part: the part index)
@@ -148,8 +152,9 @@ struct AdamHyper {
 // (sq *= gscale², sq *= sq_mul; norm = sqrt(sq); coef = min(1, max/(norm+eps))
 // * gscale * coef_mul, T:nn/utils/clip_grad.py:165-174), so it is bit-identical.
 struct ClipArgs {
-  const float* sq;     // a finished Σg² (groups == 0) or `groups` group sums, kRedSyncStride apart
+  const float* sq;     // a finished Σg² (groups == 0) or `groups` group sums, `stride` floats apart
   int32_t groups;
+  int32_t stride;      // kRedSyncStride (the plan's own sums) or 1 (gs_plan_set_clip_groups)
   float max_norm, eps;
   float sq_mul, coef_mul;  // host multipliers (ZeRO's loss scale): 1 = none
   float* out;          // [sq, coef, norm] written by workgroup 0 (nullable)
@@ -283,7 +288,7 @@ int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float
                   void* stream);
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
                       void* stream);
-int hip_sqnorm_partial(gs_plan* p, int slot, int dt, void* stream);
+int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream);
 const float* hip_plan_red_groups(const gs_plan* p);  // the 64 group sums of gs_sqnorm_partial
 float* hip_plan_red_scalar(const gs_plan* p);        // its finished Σ when red_groups == 0
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi,
@@ -310,4 +315,7 @@ int host_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gs,
               const ClipArgs* clip);
 // the clip coefficient of ClipArgs on the host (groups == 0: *sq is final)
 float host_clip_factor(const ClipArgs& c, const float* gs);
+// the device's 64-lane DPP fold (gs_kernels.hip wave_reduce) restated on the
+// host: lane l holds x[l * stride] (l < n), zeros elsewhere
+float host_wave_sum(const float* x, int n, int stride);
 }  // namespace gs

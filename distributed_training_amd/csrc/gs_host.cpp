@@ -256,8 +256,28 @@ int host_unscale_check(gs_plan* p, int s_, int dt, const float* inv, float* foun
   return GS_OK;
 }
 
+// gs_kernels.hip wave_reduce<false>: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror, row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3; lane 63.
+// A lane a step does not write adds 0 (the DPP `old` operand is the identity).
+float host_wave_sum(const float* x, int n, int stride) {
+  float v[64], t[64];
+  for (int l = 0; l < 64; ++l) v[l] = 0.f + (l < n ? x[static_cast<int64_t>(l) * stride] : 0.f);
+  auto step = [&](auto src, unsigned row_mask) {
+    for (int l = 0; l < 64; ++l) t[l] = ((row_mask >> (l >> 4)) & 1u) ? v[src(l)] : 0.f;
+    for (int l = 0; l < 64; ++l) v[l] = v[l] + t[l];
+  };
+  static const int q1[4] = {1, 0, 3, 2}, q2[4] = {2, 3, 0, 1};
+  step([](int l) { return (l & ~3) | q1[l & 3]; }, 0xFu);
+  step([](int l) { return (l & ~3) | q2[l & 3]; }, 0xFu);
+  step([](int l) { return (l & ~7) | (7 - (l & 7)); }, 0xFu);
+  step([](int l) { return (l & ~15) | (15 - (l & 15)); }, 0xFu);
+  step([](int l) { return (l & ~15) - 1; }, 0xAu);  // rows 1, 3 <- lane 15 of the row below
+  step([](int) { return 31; }, 0xCu);                // rows 2, 3 <- lane 31
+  return v[63];
+}
+
 float host_clip_factor(const ClipArgs& c, const float* gsc) {
-  float sq = c.sq[0];
+  float sq = c.groups > 0 ? host_wave_sum(c.sq, c.groups, c.stride) : c.sq[0];
   const float s = gsc ? gsc[0] : 1.f;
   if (gsc) sq = sq * (s * s);
   sq = sq * c.sq_mul;

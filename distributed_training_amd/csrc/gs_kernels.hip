@@ -136,8 +136,6 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #ifndef GS_RED_FUSE_GRID
 #define GS_RED_FUSE_GRID 2048  // workgroups of a fused reduction (r2z2 sweep: 2048 < 4096 < 8192)
 #endif
-constexpr int kRedMaxGroups = 64;
-constexpr int kRedSyncStride = 32;  // words: every counter / group sum on its own 128-B line
 constexpr int kRedSyncWords = (2 * kRedMaxGroups + 1) * kRedSyncStride;
 constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too many arrivals
 #ifndef GS_G_PACK
@@ -774,7 +772,10 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
       __hip_atomic_store(&gsums[k * kStride], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (P.red_groups_only) {
         // gs_sqnorm_partial: the group sums are the result; the clipped update
-        // on this plan folds them (clip_multiplier), no top-level hand-off
+        // on this plan folds them (clip_multiplier), no top-level hand-off.
+        // gs_sqnorm_partial_out: also contiguous in caller memory (a stream-
+        // ordered consumer: the ranks' all-reduce, then the update)
+        if (P.red_out) P.red_out[k] = gsum;
         s_role = 0;
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1179,7 +1180,7 @@ __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float*
   float sq;
   if (c.groups > 0) {
     const int l = static_cast<int>(threadIdx.x & 63);
-    const float x = l < c.groups ? c.sq[l * kRedSyncStride] : 0.f;
+    const float x = l < c.groups ? c.sq[l * c.stride] : 0.f;
     sq = wave_sum(0.f + x);
   } else {
     sq = c.sq[0];
@@ -1273,18 +1274,20 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
     const bool red = Op::kRed != 0 && (red_out || groups_only);
     int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
+    // groups_only is asked for only when the ordinary reduction would fuse too
+    // (hip_sqnorm_partial), so both fold the same R group sums of the same grid
     fused = red && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
     if (fused) cap = std::min(cap, red_grid_cap(GS_RED_FUSE_GRID));
+    // any fused reduction overwrites the group sums a gs_sqnorm_partial left
+    if (fused && !groups_only) p->red_valid = false;
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     PlanArgs a = p->args();
     a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
-    a.red_out = Op::kRed != 0 ? red_out : nullptr;
+    a.red_out = Op::kRed != 0 ? red_out : nullptr;  // groups_only: the contiguous group sums (nullable)
     a.red_acc = accumulate;
-    // groups-only: always the full 64 groups (kRedMaxGroups: one per lane of the
-    // update's fold), whatever GS_RED_FUSE says for the ordinary reductions
-    a.red_fuse = fused ? (groups_only ? kRedMaxGroups : red_fuse_groups()) : 0;
+    a.red_fuse = fused ? red_fuse_groups() : 0;
     a.red_groups_only = groups_only;
-    if (groups_only) p->red_groups = std::min(grid, kRedMaxGroups);
+    if (groups_only) p->red_groups = std::min(grid, red_fuse_groups());
     a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
     hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
   } else {
@@ -1610,15 +1613,31 @@ const float* hip_plan_red_groups(const gs_plan* p) {
 }
 float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit + kRedSyncWords; }
 
-int hip_sqnorm_partial(gs_plan* p, int slot, int dt, void* stream) {
+// Groups exactly when gs_sqnorm would run the in-kernel combine (same grid, same
+// R: GS_RED_FUSE / GS_RED_GRID overrides apply to both), so the clipped update's
+// fold equals gs_sqnorm's last step bit for bit; otherwise the combine launch
+// writes the finished Σ (red_groups = 0).  groups_out (nullable): the group sums
+// also contiguous in caller memory, or the finished Σ in groups_out[0].
+int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream) {
   DeviceGuard g(p->device);
-  const bool groups = use_chunk_engine(GS_OP_SQNORM) && !p->chunks.empty() && p->n > 0 && !p->segs.empty();
+  const int cap = std::min(p->grid_cap, red_grid_cap(SqnormOp<GS_PACK_N, GS_F32>::kRedGrid));
+  const bool groups = use_chunk_engine(GS_OP_SQNORM) && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
+                      red_fuse_groups() > 0 && cap <= kRedFuseMaxGrid;
   GS_DISPATCH_FLOAT(dt, DT, {
     SqnormOp<GS_PACK_N, DT> op;
     op.slot = slot;
-    if (groups) return launch<GS_RED_ILP>(p, op, stream, nullptr, 0, 1);
+    if (groups) {
+      GS_TRY_RET(launch<GS_RED_ILP>(p, op, stream, groups_out, 0, 1));
+      if (n_groups) *n_groups = p->red_groups;
+      return GS_OK;
+    }
     p->red_groups = 0;
-    return launch<GS_RED_ILP>(p, op, stream, hip_plan_red_scalar(p), 0);
+    if (n_groups) *n_groups = 1;
+    GS_TRY_RET(launch<GS_RED_ILP>(p, op, stream, hip_plan_red_scalar(p), 0));
+    if (groups_out)
+      HIP_RET(hipMemcpyAsync(groups_out, hip_plan_red_scalar(p), sizeof(float), hipMemcpyDeviceToDevice,
+                             static_cast<hipStream_t>(stream)));
+    return GS_OK;
   });
   return GS_OK;
 }

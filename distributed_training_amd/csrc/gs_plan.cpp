@@ -364,7 +364,24 @@ int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream) {
     p->red_groups = 0;
     return host_sqnorm(p, slot, dtype, &p->h_red, 0);
   }
-  return hip_sqnorm_partial(p, slot, dtype, stream);
+  return hip_sqnorm_partial(p, slot, dtype, nullptr, nullptr, stream);
+}
+
+int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, int32_t* n_groups,
+                          void* stream) {
+  GsRange range("gs_sqnorm_partial_out");
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(groups_out != nullptr && n_groups != nullptr, "gs_sqnorm_partial_out: NULL argument");
+  p->red_valid = true;
+  if (p->kind == GS_DEV_HOST) {
+    p->red_groups = 0;
+    GS_TRY_RET(host_sqnorm(p, slot, dtype, &p->h_red, 0));
+    groups_out[0] = p->h_red;
+    *n_groups = 1;
+    return GS_OK;
+  }
+  return hip_sqnorm_partial(p, slot, dtype, groups_out, n_groups, stream);
 }
 
 int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
@@ -377,7 +394,23 @@ int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float 
   GS_CHECK_ARG(eps >= 0.f, "gs_plan_set_clip: eps < 0");
   p->clip_on = true;
   p->clip_own = sqnorm_dev == nullptr;
-  p->clip = ClipArgs{sqnorm_dev, 0, max_norm, eps, sq_mul, coef_mul, out_dev};
+  p->clip = ClipArgs{sqnorm_dev, 0, 1, max_norm, eps, sq_mul, coef_mul, out_dev};
+  return GS_OK;
+}
+
+int gs_plan_set_clip_groups(gs_plan* p, const float* groups_dev, int32_t n_groups, float max_norm,
+                            float eps, float sq_mul, float coef_mul, float* out_dev) {
+  PLAN_OK(p);
+  if (!(max_norm > 0.f)) {
+    p->clip_on = false;
+    return GS_OK;
+  }
+  GS_CHECK_ARG(groups_dev != nullptr, "gs_plan_set_clip_groups: NULL group sums");
+  GS_CHECK_ARG(n_groups >= 1 && n_groups <= GS_RED_GROUPS, "gs_plan_set_clip_groups: n_groups out of 1..64");
+  GS_CHECK_ARG(eps >= 0.f, "gs_plan_set_clip_groups: eps < 0");
+  p->clip_on = true;
+  p->clip_own = false;
+  p->clip = ClipArgs{groups_dev, n_groups, 1, max_norm, eps, sq_mul, coef_mul, out_dev};
   return GS_OK;
 }
 
@@ -387,13 +420,19 @@ static int plan_clip(gs_plan* p, ClipArgs* c, const ClipArgs** out) {
   if (!p->clip_on) return GS_OK;
   *c = p->clip;
   if (p->clip_own) {
+    // the plan's own partial sums serve ONE update: a later update without a fresh
+    // gs_sqnorm_partial fails instead of clipping with stale sums (and any other
+    // fused reduction on the plan in between overwrote them: gs_kernels.hip launch)
     if (!p->red_valid)
-      return fail(GS_ESTATE, "clipped update from the plan's own Σg²: call gs_sqnorm_partial first");
+      return fail(GS_ESTATE, "clipped update from the plan's own Σg²: call gs_sqnorm_partial first "
+                             "(once per update; a fused reduction on the plan in between overwrites it)");
+    p->red_valid = false;
     if (p->kind == GS_DEV_HOST) {
       c->sq = &p->h_red;
       c->groups = 0;
     } else {
       c->groups = p->red_groups;
+      c->stride = kRedSyncStride;
       c->sq = p->red_groups > 0 ? hip_plan_red_groups(p) : hip_plan_red_scalar(p);
     }
   }

@@ -205,7 +205,22 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
     }
   }
 
+  // static_graph DDP: a parameter the (fixed) graph never uses is marked ready at
+  // the end of backward, as torch's static-graph Reducer does (ddp.py
+  // _finalize_backward's static_graph branch); its slot reduces as zeros
+  void set_mark_unused(bool on) { mark_unused_ = on; }
+
   void finalize() {
+    if (mark_unused_) {
+      int32_t n_ready = 0;
+      const int ru = gs_bucketer_mark_unused(b_, stream_, ready_.data(), &n_ready);
+      if (ru < 0) {
+        in_backward_ = false;
+        finalize_queued_ = false;
+        pinned_.clear();
+        throw std::runtime_error(std::string("gs_bucketer_mark_unused: ") + gs_last_error());
+      }
+    }
     const int rc = gs_bucketer_finalize(b_, stream_);
     in_backward_ = false;
     finalize_queued_ = false;
@@ -252,6 +267,7 @@ class Hooks : public std::enable_shared_from_this<Hooks> {
   void* stream_ = nullptr;
   bool in_backward_ = false, finalize_queued_ = false, record_order_ = false;
   bool release_ = false;
+  bool mark_unused_ = false;
   std::vector<int> bucket_of_;
   std::vector<std::vector<at::Tensor>> held_;
   void* comm_stream_ = nullptr;
@@ -275,6 +291,7 @@ PYBIND11_MODULE(_gshook, m) {
       .def("attached", &Hooks::attached)
       .def("set_bucketer", &Hooks::set_bucketer, py::arg("handle"), py::arg("n_buckets"),
            py::arg("bucket_of") = std::vector<int>(), py::arg("comm_stream") = 0)
+      .def("set_mark_unused", &Hooks::set_mark_unused)
       .def("prepare", &Hooks::prepare)
       .def("order", &Hooks::order)
       .def("in_backward", &Hooks::in_backward)

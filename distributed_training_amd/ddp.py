@@ -452,6 +452,9 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._native_on = False
         if self._native is not None:
             self._native.set_bucketer(self._bucketer.handle.value, len(self._bucketer.buckets))
+            # static_graph: the C++ finalize marks never-used parameters ready first,
+            # as _finalize_backward's static_graph branch does on the Python hooks
+            self._native.set_mark_unused(bool(self.static_graph))
         self._set_native(self._native_ok())
 
     # ------------------------------------------------------------------ setup

@@ -159,6 +159,33 @@ class TensorListPlan:
         L.check(L.lib().gs_sqnorm_partial(self.handle, slot, L.gs_dtype(dtype), self._stream(stream)),
                 "gs_sqnorm_partial")
 
+    def sqnorm_partial_out(self, slot, dtype, groups: torch.Tensor, stream=None) -> int:
+        """:meth:`sqnorm_partial` whose group sums also land contiguously in
+        ``groups`` (fp32, >= 64 elements, where the plan runs; gs_sqnorm_partial_out);
+        returns how many are valid.  Sharded optimizers SUM-all-reduce
+        ``groups[:n]`` across ranks, then :meth:`set_clip_groups`."""
+        if groups.dtype != torch.float32 or groups.numel() < L.GS_RED_GROUPS or not groups.is_contiguous() or \
+                (groups.device.type == "cuda") != (self.kind == L.GS_DEV_HIP):
+            raise ValueError(f"group sums: contiguous fp32[>= {L.GS_RED_GROUPS}] where the plan runs")
+        n = ctypes.c_int32()
+        L.check(L.lib().gs_sqnorm_partial_out(self.handle, slot, L.gs_dtype(dtype), groups.data_ptr(),
+                                              ctypes.byref(n), self._stream(stream)), "gs_sqnorm_partial_out")
+        return n.value
+
+    def set_clip_groups(self, max_norm: float | None, eps: float, groups: torch.Tensor, n_groups: int,
+                        sq_mul: float = 1.0, coef_mul: float = 1.0, out: torch.Tensor | None = None):
+        """:meth:`set_clip` with ‖g‖² = the fold of ``groups[:n_groups]``
+        (gs_plan_set_clip_groups), the update's workgroups folding them."""
+        for t in (groups, out):
+            if t is not None and (t.dtype != torch.float32 or (t.device.type == "cuda") != (self.kind == L.GS_DEV_HIP)):
+                raise ValueError("clip tensors: fp32, where the plan runs")
+        if out is not None and out.numel() < 3:
+            raise ValueError("clip out: 3 elements")
+        L.check(L.lib().gs_plan_set_clip_groups(self.handle, groups.data_ptr(), int(n_groups), float(max_norm or 0.0),
+                                                float(eps), float(sq_mul), float(coef_mul),
+                                                None if out is None else out.data_ptr()), "gs_plan_set_clip_groups")
+        self._clip_refs = (groups, out)
+
     def set_clip(self, max_norm: float | None, eps: float = 1e-6, sqnorm: torch.Tensor | None = None,
                  sq_mul: float = 1.0, coef_mul: float = 1.0, out: torch.Tensor | None = None):
         """Fold the clip coefficient min(1, max_norm/(‖g‖+eps)) into the later

@@ -12,8 +12,9 @@ one bucket for ResNet-18/50):
 backward: hooks pack each bucket and RCCL reduce-scatters it (stage 2) or
           all-reduces it (stage 1) on libgsync's stream, under backward;
 step:     (fp16) non-finite check of the shard + MAX all-reduce of the flag,
-          (clip) Σg² of the shard + SUM all-reduce of one fp32 scalar,
-          coefficient on device; ONE fused Adam/SGD launch over all shards
+          (clip) Σg² group sums of the shard + one SUM all-reduce of those
+          <= 64 floats, folded into the update (no combine / coefficient
+          launch); ONE fused Adam/SGD launch over all shards
           that also writes the low-precision params into this rank's slice
           of the param flat buffer; in-place all-gather of each bucket.
 No host synchronisation except the fp16 loss-scale bookkeeping (DeepSpeed
@@ -140,6 +141,8 @@ class ZeroDataParallel:
         self._pending = {}
         # [found_inf, Σg² (all-reduced), 1/scale, -, clip out: Σg²·s², coefficient, ‖g‖]
         self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
+        # world > 1 folded clip: this rank's Σg² group sums, then their SUM over ranks
+        self._red_groups = torch.zeros(L.GS_RED_GROUPS, dtype=torch.float32, device=self.device)
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
         # the per-gradient hook in C++ (_gshook, release mode: the grad is freed once its
         # pack is enqueued) on the library-collective path; Python hooks otherwise
@@ -351,16 +354,20 @@ class ZeroDataParallel:
         if self.clip > 0 and _optim.CLIP_FUSED:
             # DeepSpeed gradient_clipping (R:resnet/deepspeed/deepspeed_train.py:195) folded
             # into the update: its workgroups form min(1, c/(‖g‖+1e-6))·(1/scale) themselves
-            # (gs_plan_set_clip) — no coefficient launch; one rank: Σg² stays as the plan's
-            # partial sums (no combine launch either)
+            # (gs_plan_set_clip) — no combine launch, no coefficient launch
             if self.world == 1:
+                # Σg² stays as the plan's partial sums
                 self.plan.sqnorm_partial(1, self.dtype)
                 self.plan.set_clip(self.clip, 1e-6, None, inv_scale * inv_scale, inv_scale, out=s[4:7])
             else:
-                sq = s[1:2]
-                self.plan.sqnorm(1, self.dtype, sq)
-                self._allreduce_scalar(sq, "sum")
-                self.plan.set_clip(self.clip, 1e-6, sq, inv_scale * inv_scale, inv_scale, out=s[4:7])
+                # this shard's group sums (<= 64 floats) SUM-all-reduced over the ranks (one
+                # message, identical bits everywhere), folded by every update workgroup:
+                # Σg² kernel -> 256-B collective -> update, nothing in between (DeepSpeed:
+                # per-rank Σ, scalar all_reduce, coefficient, U)
+                gr = self._red_groups
+                n = self.plan.sqnorm_partial_out(1, self.dtype, gr)
+                self._allreduce_scalar(gr[:n], "sum")
+                self.plan.set_clip_groups(self.clip, 1e-6, gr, n, inv_scale * inv_scale, inv_scale, out=s[4:7])
         elif self.clip > 0:
             self.plan.set_clip(None)
             sq = s[1:2]

@@ -10,6 +10,7 @@ CPU tests run the host backend; the `gpu` ones the gfx950 kernels, where the
 folded coefficient comes from the Σg² kernel's 64 group sums."""
 from __future__ import annotations
 
+import numpy as np
 import pytest
 import torch
 
@@ -148,6 +149,81 @@ def test_plan_clip_needs_partial_first():
     assert torch.equal(p, torch.full((8,), 1.0) * coef * -0.1)
 
 
+def test_plan_clip_partial_is_single_use():
+    """the plan's own Σg² partial feeds ONE clipped update; a second
+    update without a fresh gs_sqnorm_partial fails (GS_ESTATE) instead of
+    clipping with stale sums."""
+    plan = D.multi_tensor.TensorListPlan([8], torch.device("cpu"), task_units=0)
+    p, g, b = torch.zeros(8), torch.ones(8), torch.zeros(8)
+    for k, t in enumerate((p, g, b)):
+        plan.set_ptrs(k, [t])
+    plan.sqnorm_partial(1, torch.float32)
+    plan.set_clip(1.0)
+    plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    with pytest.raises(D._lib.GsyncError, match="gs_sqnorm_partial"):
+        plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    plan.sqnorm_partial(1, torch.float32)
+    plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+
+
+def _dpp_wave_sum(x):
+    """The update kernel's 64-lane fold (gs_kernels.hip wave_reduce), restated
+    independently: quad_perm [1,0,3,2] / [2,3,0,1] and the half-row / row
+    mirrors are lane XORs 1 / 2 / 7 / 15; row_bcast:15 adds lane 15 of the row
+    below into rows 1 and 3, row_bcast:31 adds lane 31 into rows 2 and 3."""
+    lanes = np.arange(64)
+    v = np.zeros(64, np.float32)
+    v[:len(x)] = np.asarray(x, np.float32)
+
+    def step(v, src, rows):
+        t = np.zeros(64, np.float32)
+        m = np.isin(lanes // 16, rows)
+        t[m] = v[src[m]]
+        return (v + t).astype(np.float32)
+
+    for mask in (1, 2, 7, 15):
+        v = step(v, lanes ^ mask, [0, 1, 2, 3])
+    v = step(v, (lanes // 16) * 16 - 1, [1, 3])
+    v = step(v, np.full(64, 31), [2, 3])
+    return v[63]
+
+
+@pytest.mark.parametrize("n", [1, 5, 64])
+def test_clip_groups_fold_host(n):
+    """gs_plan_set_clip_groups on a host plan: the published Σg² is the device
+    fold of the group sums (restated above), coefficient and update follow."""
+    g0 = torch.Generator().manual_seed(n)
+    groups = torch.rand(64, generator=g0) * 100.0
+    plan = D.multi_tensor.TensorListPlan([16], torch.device("cpu"), task_units=0)
+    p, g, b = torch.zeros(16), torch.ones(16), torch.zeros(16)
+    for k, t in enumerate((p, g, b)):
+        plan.set_ptrs(k, [t])
+    out = torch.zeros(3)
+    plan.set_clip_groups(1.0, 1e-6, groups, n, out=out)
+    plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    sq = np.float32(_dpp_wave_sum(groups[:n].numpy()))
+    assert out[0].item() == float(sq)
+    nrm = np.sqrt(sq, dtype=np.float32)
+    coef = min(np.float32(1.0) / (nrm + np.float32(1e-6)), np.float32(1.0))
+    assert out[1].item() == float(coef) and out[2].item() == float(nrm)
+    want = np.float32(-0.1) * np.float32(np.float32(1.0) * coef)  # fmaf(-lr, g·coef, 0)
+    assert torch.equal(p, torch.full((16,), float(want)))
+    with pytest.raises(D._lib.GsyncError, match="n_groups"):
+        plan.set_clip_groups(1.0, 1e-6, groups, 65)
+
+
+def test_sqnorm_partial_out_host():
+    """Host plans: one group, the finished Σg² (what gs_sqnorm gives)."""
+    xs = [torch.randn(n, generator=torch.Generator().manual_seed(n)) for n in (7, 1000, 33)]
+    plan = D.multi_tensor.TensorListPlan([x.numel() for x in xs], torch.device("cpu"), task_units=0)
+    plan.set_ptrs(1, xs)
+    gr = torch.zeros(64)
+    n = plan.sqnorm_partial_out(1, torch.float32, gr)
+    ref = torch.zeros(1)
+    plan.sqnorm(1, torch.float32, ref)
+    assert n == 1 and gr[0].item() == ref.item()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("opt_cls,kw", CASES)
 @pytest.mark.parametrize("gscale", [None, 0.125])
@@ -193,3 +269,65 @@ def test_folded_clip_large_plan_gpu(mixed):
     for x, y in zip(res[0][0], res[1][0]):
         assert torch.equal(x, y)
     assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.gpu
+def test_clip_groups_fold_gpu_equals_host_and_sqnorm():
+    """The device fold of gs_plan_set_clip_groups == the host restatement bit for
+    bit (64, 5 and 1 random group sums); gs_sqnorm_partial_out's group sums of a
+    ResNet-50-sized slot folded == gs_sqnorm's Σg² bit for bit."""
+    dev = torch.device("cuda", 0)
+    for n in (64, 5, 1):
+        groups = torch.rand(64, generator=torch.Generator().manual_seed(n)) * 100.0
+        outs = []
+        for d in (dev, torch.device("cpu")):
+            plan = D.multi_tensor.TensorListPlan([4096], d, task_units=0)
+            p, g, b = (torch.zeros(4096, device=d), torch.ones(4096, device=d), torch.zeros(4096, device=d))
+            for k, t in enumerate((p, g, b)):
+                plan.set_ptrs(k, [t])
+            out = torch.zeros(3, device=d)
+            plan.set_clip_groups(1.0, 1e-6, groups.to(d), n, out=out)
+            plan.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+            outs.append((out.cpu(), p.cpu()))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), n
+        assert outs[1][0][0].item() == float(np.float32(_dpp_wave_sum(groups[:n].numpy())))
+    sizes = [2048 * 1000, 1000, 512 * 2048, 2048, 2048 * 512 * 9, 64 * 3 * 49, 7, 2048 * 4096]
+    gen = torch.Generator(device=dev).manual_seed(9)
+    xs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
+    plan = D.multi_tensor.TensorListPlan(sizes, dev)
+    plan.set_ptrs(1, xs)
+    gr = torch.zeros(64, device=dev)
+    n = plan.sqnorm_partial_out(1, torch.float32, gr)
+    ref = torch.zeros(1, device=dev)
+    plan.sqnorm(1, torch.float32, ref)
+    torch.cuda.synchronize()
+    assert n == 64
+    assert float(np.float32(_dpp_wave_sum(gr.cpu().numpy()[:n]))) == ref.item()
+
+
+_RED_FUSE_CHILD = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+from tests.test_clip_fold import _run, _assert_same, CASES
+dev = torch.device("cuda", 0)
+for opt_cls, kw in CASES:
+    _assert_same(_run(dev, True, opt_cls, kw, None), _run(dev, False, opt_cls, kw, None))
+print("OK")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"GS_RED_FUSE": "16"}, {"GS_RED_FUSE": "0"}, {"GS_RED_GRID": "512"}])
+def test_folded_clip_equals_separate_path_reduction_overrides_gpu(env):
+    """the folded clip follows the reduction settings gs_sqnorm uses
+    (GS_RED_FUSE groups, or the combine launch at GS_RED_FUSE=0; GS_RED_GRID), so
+    it stays bit-identical to the separate path under the A/B sweeps' overrides
+    (read once per process: a child process per setting)."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _RED_FUSE_CHILD.format(repo=repo)], env={**os.environ, **env},
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

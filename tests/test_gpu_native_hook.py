@@ -87,3 +87,41 @@ def test_native_hooks_grads_equal_local_grads(cuda_device, rccl_pg, opt_name):
 
     maps = collections.OrderedDict((ln.split()[-1], 1) for ln in open("/proc/self/maps") if "_gshook" in ln)
     assert any(m.endswith("distributed_training_amd/lib/_gshook.so") for m in maps), list(maps)
+
+
+def test_native_hooks_static_graph_never_used_parameter(cuda_device, rccl_pg):
+    """static_graph=True with a module the graph never uses, on the C++ hooks
+    (their finalize skipped gs_bucketer_mark_unused and raised
+    'Expected to have finished reduction'): three iterations; grads equal the
+    local grads snapshotted before the pack (ws=1) and torch DDP's None for the
+    never-used layer; the Python-hook path gives the same."""
+    import distributed_training_amd as D
+    from tests.test_ddp_cpu import _Branchy
+
+    for native in (True, False):
+        torch.manual_seed(0)
+        m = _Branchy().to(cuda_device)
+        params = list(m.parameters())
+        local = {}
+        for i, p in enumerate(params):
+            p.register_post_accumulate_grad_hook(lambda q, i=i: local.__setitem__(i, q.grad.detach().clone()))
+        ddp = D.DistributedDataParallel(m, static_graph=True)
+        if not native:
+            ddp._native = None
+            ddp._set_native(False)
+        g = torch.Generator(device=cuda_device).manual_seed(11)
+        for it in range(3):
+            for p in params:
+                p.grad = None
+            local.clear()
+            x = torch.rand(4, 3, 32, 32, device=cuda_device, generator=g)
+            y = torch.randint(0, 10, (4,), device=cuda_device, generator=g)
+            torch.nn.functional.cross_entropy(ddp(x, True), y).backward()
+            assert ddp._native_on == native
+            for i, p in enumerate(params):
+                if i in local:
+                    assert torch.equal(p.grad, local[i]), f"native={native} it {it} param {i}"
+                else:
+                    assert p.grad is None, f"native={native} it {it} param {i}: never used"
+        assert m.dead.weight.grad is None and m.extra.weight.grad is not None
+        torch.cuda.synchronize()

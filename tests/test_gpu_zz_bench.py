@@ -72,6 +72,14 @@ def _check_line(d, n):
     assert k["kernels"]["clip_path_sgd"]["avg_ms"] > k["kernels"]["sgd_momentum_wd"]["avg_ms"]
     assert all(r["GBps"] > 0 and abs(r["frac"] - r["GBps"] / 8000.0) < 1e-12 for r in k["kernels"].values())
     assert k["params"] == d["config"]["params"]
+    # the same rows on a > 256 MiB working set (true HBM), and the headline kernel's rate there
+    b = k["beyond_ic"]
+    assert set(b["kernels"]) == set(k["kernels"]) and b["params"] > 100_000_000
+    assert abs(r["frac_beyond_ic"] - b["kernels"]["sgd_momentum_wd"]["frac"]) < 1e-12
+    if n == 1:  # configs[3]'s N>1 clip path at its N=8 shard, over the one-rank RCCL communicator
+        z, zs = k["clip_path_zero_n8"], k["clip_path_zero_n8_scalar"]
+        assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > z["kernels_ms"] > 0
+        assert zs["avg_ms"] > 0 and z["vs_scalar_form"] > 0
     # the self-check step after the timed region (distributed_training_amd/parity.py)
     p = d["parity"]
     assert p is not None and p["ok"] is True and p["world"] == n, p
@@ -216,18 +224,36 @@ def test_bench_multirank_gloo_rehearsal(cuda_device, engine, n):
         assert par["buffers_identical"] is True
 
 
-def test_bench_leg_watchdog_keeps_the_headline(cuda_device):
-    """N>1: optional legs that overrun --leg-budget-s (here: 1 s, so the first
-    leg overruns) end every rank with exit 0 after rank 0 printed the line —
-    the headline and roofline intact, the unfinished leg named."""
+def test_bench_wall_budget_skips_legs_keeps_the_headline(cuda_device):
+    """N>1 with a wall budget already spent by warm-up (1 s): every optional leg
+    is skipped and named in leg_errors, the headline and roofline intact, exit 0."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--leg-budget-s", "1", "--kernel-rates", "0",
+           "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--wall-budget-s", "1", "--kernel-rates", "0",
            "--policy-ab", "1"] + SMALL
     p = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=500)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]
     d = lines[0]
-    assert d["legs_incomplete"]["budget_s"] == 1.0 and d["legs_incomplete"]["leg"] != "done"
+    assert d["value"] > 0 and d["roofline"]["achieved"] > 0 and d["n_gpus"] == 2
+    skipped = {k for k, v in d["leg_errors"].items() if v.startswith("skipped")}
+    assert {"tail_split", "parity", "collective_bench", "zero2", "colossal", "bucket_policy_ab"} <= skipped, skipped
+    assert "legs_incomplete" not in d
+
+
+def test_bench_leg_watchdog_exits_nonzero_keeps_the_headline(cuda_device):
+    """N>1: a leg still running past the wall budget (a hung collective; here the
+    test hook GSYNC_BENCH_TEST_HANG_LEG) ends every rank with exit status 3 after
+    rank 0 printed the line — the headline and roofline intact, the leg named."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--wall-budget-s", "1", "--kernel-rates", "0"] + SMALL
+    env = dict(_env(), GSYNC_BENCH_TEST_HANG_LEG="parity")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=500)
+    assert p.returncode != 0, "a leg overrunning the budget must not look like a clean run"
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = lines[0]
+    assert d["legs_incomplete"] == {"leg": "parity", "wall_budget_s": 1.0}
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0 and d["n_gpus"] == 2

@@ -24,6 +24,7 @@ def _force_native(ddp):
     ref = weakref.ref(ddp)
     ddp._native = L.hook_module().Hooks(ddp._params, -1, lambda: ref()._native_finalized())
     ddp._native.set_bucketer(ddp._bucketer.handle.value, len(ddp._bucketer.buckets))
+    ddp._native.set_mark_unused(bool(ddp.static_graph))
     ddp._native_ok = lambda: ddp._capture_local is None  # host bucketer: no library collective
     ddp._set_native(True)
 
@@ -125,3 +126,40 @@ def _zero_native_vs_python(rank, ws):
 
 def test_native_hooks_zero_release_mode_ws1():
     _run(_zero_native_vs_python, 1)
+
+
+def _native_static_graph(rank, ws):
+    """static_graph=True with a never-used layer on the C++ hooks: their finalize
+    marks it ready (gs_bucketer_mark_unused) as the Python _finalize_backward does;
+    grads equal torch's static-graph DDP bit for bit, the dead layer's stay None."""
+    import distributed_training_amd as D
+    from tests.test_ddp_cpu import _Branchy
+
+    out = {}
+    for impl in ("torch", "native"):
+        torch.manual_seed(0)
+        m = _Branchy()
+        if impl == "torch":
+            ddp = torch.nn.parallel.DistributedDataParallel(m, static_graph=True)
+        else:
+            ddp = D.DistributedDataParallel(m, static_graph=True)
+            _force_native(ddp)
+        g = torch.Generator().manual_seed(7)
+        res = []
+        for _ in range(3):
+            for p in m.parameters():
+                p.grad = None
+            x = torch.rand(4, 3, 32, 32, generator=g)
+            y = torch.randint(0, 10, (4,), generator=g)
+            nn.functional.cross_entropy(ddp(x, True), y).backward()
+            res.append([None if p.grad is None else p.grad.clone() for p in m.parameters()])
+        if impl == "native":
+            assert ddp._native_on
+        out[impl] = res
+    for it, (a, b) in enumerate(zip(out["torch"], out["native"])):
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert (u is None) == (v is None) and (u is None or torch.equal(u, v)), f"iter {it} param {i}"
+
+
+def test_native_hooks_static_graph_ws1():
+    _run(_native_static_graph, 1)
