@@ -104,6 +104,10 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #ifndef GS_NT_LOAD
 #define GS_NT_LOAD 0
 #endif
+// non-temporal loads for the updates' read-once gradient stream only
+#ifndef GS_NT_LOAD_GRAD
+#define GS_NT_LOAD_GRAD GS_NT_LOAD
+#endif
 #ifndef GS_NT_STORE
 #define GS_NT_STORE 1
 #endif
@@ -167,13 +171,10 @@ constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too 
 #define GS_SGPR_ATTR
 #endif
 
-template <class V>
+template <bool NT = (GS_NT_LOAD != 0), class V>
 __device__ __forceinline__ V vload(const GLOBAL_AS V* p) {
-#if GS_NT_LOAD
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
 }
 template <class V>
 __device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
@@ -187,7 +188,7 @@ __device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
 // load N (4 or 8) consecutive elements [e, e+N) of a tensor with n elements;
 // e is a multiple of N.  fp32: N/4 16-B loads; 16-bit: one 8-B (N=4) or
 // 16-B (N=8) load.  `vec`: the tensor base is 16-B aligned.
-template <int DT, int N>
+template <int DT, int N, bool NT = (GS_NT_LOAD != 0)>
 __device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bool vec,
                                       float (&x)[N]) {
   static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
@@ -196,7 +197,7 @@ __device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bo
     if (vec && e + N <= n) {
 #pragma unroll
       for (int h = 0; h < N / 4; ++h) {
-        const gf4 v = vload((const GLOBAL_AS gf4*)(p + 4 * h));
+        const gf4 v = vload<NT>((const GLOBAL_AS gf4*)(p + 4 * h));
         x[4 * h + 0] = v.x; x[4 * h + 1] = v.y; x[4 * h + 2] = v.z; x[4 * h + 3] = v.w;
       }
     } else {
@@ -208,10 +209,10 @@ __device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bo
     if (vec && e + N <= n) {
       uint32_t w[N / 2];
       if constexpr (N == 8) {
-        const gu4 v = vload((const GLOBAL_AS gu4*)p);
+        const gu4 v = vload<NT>((const GLOBAL_AS gu4*)p);
         w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
       } else {
-        const gu2 v = vload((const GLOBAL_AS gu2*)p);
+        const gu2 v = vload<NT>((const GLOBAL_AS gu2*)p);
         w[0] = v.x; w[1] = v.y;
       }
 #pragma unroll
@@ -277,13 +278,13 @@ template <int DT>
 __device__ __forceinline__ const void* elem_at(const void* base, int64_t e0) {
   return static_cast<const char*>(base) + e0 * (DT == GS_F32 ? 4 : 2);
 }
-template <int DT>
+template <int DT, bool NT = (GS_NT_LOAD != 0)>
 __device__ __forceinline__ void load4F(const void* base, uint32_t lo, float (&x)[4]) {
   if constexpr (DT == GS_F32) {
-    const gf4 v = vload((const GLOBAL_AS gf4*)(gptr<float>(base) + lo));
+    const gf4 v = vload<NT>((const GLOBAL_AS gf4*)(gptr<float>(base) + lo));
     x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
   } else {
-    const gu2 v = vload((const GLOBAL_AS gu2*)(gptr<uint16_t>(base) + lo));
+    const gu2 v = vload<NT>((const GLOBAL_AS gu2*)(gptr<uint16_t>(base) + lo));
     x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
     x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
     x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
@@ -305,14 +306,14 @@ __device__ __forceinline__ void store4F(void* base, uint32_t lo, const float (&x
 }
 // F = full-chunk fast path (above); otherwise element e0 + lo of a tensor of
 // n elements with the bounds / alignment checks of loadN / storeN
-template <int DT, int N, bool F>
+template <int DT, int N, bool F, bool NT = (GS_NT_LOAD != 0)>
 __device__ __forceinline__ void ld(const void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
                                    float (&x)[N]) {
   if constexpr (F) {
     static_assert(N == 4, "the chunk engine moves 4 elements per lane-access");
-    load4F<DT>(elem_at<DT>(base, e0), lo, x);
+    load4F<DT, NT>(elem_at<DT>(base, e0), lo, x);
   } else {
-    loadN<DT, N>(base, e0 + lo, n, vec, x);
+    loadN<DT, N, NT>(base, e0 + lo, n, vec, x);
   }
 }
 template <int DT, int N, bool F>
@@ -1089,7 +1090,7 @@ struct SgdOp {
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
     ld<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
-    ld<GD, N, F>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
+    ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
     if (h.mom != 0.f && !h.first) ld<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
   template <bool F>
@@ -1141,7 +1142,7 @@ struct AdamOp {
   template <bool F>
   __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
     ld<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
-    ld<GD, N, F>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
+    ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
     ld<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
     ld<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }

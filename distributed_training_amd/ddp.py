@@ -1416,9 +1416,19 @@ class _DDPJoinHook(JoinHook):
     def main_hook(self):
         d = self.ddp
         d._maybe_rebuild_buckets()
-        if d._will_sync_module_buffers():
+        # the training ranks' forward, collective for collective: the buffer sync before
+        # the module (common-rank pick + broadcast, or a PRE_FORWARD buffer comm hook),
+        # the sync flag, then a POST_FORWARD buffer comm hook after the module (torch
+        # leaves buffer comm hooks under join unsupported, pytorch#65436)
+        bh = d.buffer_hook
+        post_fwd = bh is not None and bh.buffer_comm_hook_location == _BufferCommHookLocation.POST_FORWARD
+        sync_bufs = d._will_sync_module_buffers()
+        if sync_bufs and not post_fwd:
             d._sync_buffers(d._find_common_rank(d.rank, False))
         should_sync = d._check_global_requires_backward_grad_sync(is_joined_rank=True)
+        if sync_bufs and post_fwd:
+            d._sync_buffers()
+            d._wait_post_backward_futures()  # no backward here to await the hook's futures
         d.require_forward_param_sync = should_sync
         if not should_sync:
             return

@@ -25,7 +25,23 @@ def test_bench_defaults_parse():
     assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]
 
 
-@pytest.mark.parametrize("script", ["gpu_round.sh", "gpu_tests.sh", "r2_tail.sh", "red_sweep.sh"])
+@pytest.mark.parametrize("script", sorted(f for f in os.listdir(os.path.join(REPO, "scripts")) if f.endswith(".sh")))
 def test_gpu_scripts_parse(script):
     p = subprocess.run(["bash", "-n", os.path.join(REPO, "scripts", script)], capture_output=True, text=True)
     assert p.returncode == 0, p.stderr
+
+
+def test_every_script_is_cited():
+    """Each script kept under scripts/ is cited by DESIGN.md, README.md or a test
+    (one-offs that are not go to scripts/archive/, provenance of older profiles)."""
+    import glob
+    import re
+
+    text = "".join(open(os.path.join(REPO, f)).read() for f in ("DESIGN.md", "README.md", "INTEGRATION.md", "bench.py"))
+    text += "".join(open(f).read() for f in glob.glob(os.path.join(REPO, "tests", "*.py")))
+    text += "".join(open(f).read() for f in glob.glob(os.path.join(REPO, "scripts", "*.sh")))
+    for f in sorted(os.listdir(os.path.join(REPO, "scripts"))):
+        path = os.path.join(REPO, "scripts", f)
+        if os.path.isdir(path) or f.startswith("."):
+            continue
+        assert re.search(r"(?<![A-Za-z0-9_])" + re.escape(f), text), f"scripts/{f} is cited nowhere"

@@ -285,6 +285,54 @@ def test_buffer_comm_hook_matches_torch(where):
     _run(_buffer_hook, 2, where)
 
 
+def _join_buffer_hook(rank, ws, where):
+    """ddp.join() with uneven inputs and a buffer comm hook (the joined
+    ranks' shadow of a forward must issue the training ranks' collectives in the
+    same order; a POST_FORWARD hook used to leave them mismatched).  Rank r runs
+    2 + 2r batches; the run completes, the hook runs once per iteration of the
+    longest rank on every rank, and the final model is the same on every rank."""
+    import distributed_training_amd as D
+    from torch.nn.parallel.distributed import _BufferCommHookLocation as Loc
+
+    torch.manual_seed(0)
+    m = _micro()
+    a = D.DistributedDataParallel(m, bucket_cap_mb=0.01)
+    calls = []
+
+    def hook(state, named):
+        calls.append(len(named))
+        # in place, outside autograd's version counter (BN saved its stats for backward)
+        futs = [dist.all_reduce(t, async_op=True).get_future() for t in named.values() if t.is_floating_point()]
+        if where == "PRE_FORWARD":
+            torch.futures.wait_all(futs)
+            return None
+        return futs
+
+    a._register_buffer_comm_hook(None, hook, getattr(Loc, where))
+    opt = torch.optim.SGD(a.parameters(), lr=0.05)
+    g = torch.Generator().manual_seed(40 + rank)
+    batches = [(torch.rand(3, 3, 32, 32, generator=g), torch.randint(0, 10, (3,), generator=g))
+               for _ in range(2 + 2 * rank)]
+    with a.join():
+        for x, y in batches:
+            opt.zero_grad()
+            nn.functional.cross_entropy(a(x), y).backward()
+            opt.step()
+    # the longest rank ran 2 + 2(ws-1) iterations and every rank called the hook once per
+    # iteration (joined ranks shadowing the rest)
+    assert len(calls) == 2 + 2 * (ws - 1), calls
+    for t in m.state_dict().values():
+        lo, hi = t.double().clone(), t.double().clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        assert torch.equal(lo, hi)
+
+
+@pytest.mark.parametrize("where", ["PRE_FORWARD", "POST_FORWARD"])
+def test_join_with_buffer_comm_hook(where):
+    _run(_join_buffer_hook, 2, where)
+
+
 def _uneven(rank, ws, opt_name, divide_initial=True):
     """ddp.join() with uneven inputs (rank r has 2 + 2r batches): the same
     weights, BN buffers and per-iteration grads as torch's DDP under its own
