@@ -318,24 +318,49 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
         plan.set_clip(1.0, 1e-6, sq, out=out)
         adam()
 
-    rows = {}
-    for name, fn in (("clip_path_zero_n8", folded), ("clip_path_zero_n8_scalar", scalar)):
-        for _ in range(3):
-            fn()
+    # The step's end runs behind backward's queued kernels, so the host enqueues these
+    # launches ahead of the GPU: time them the same way, behind a spin kernel long
+    # enough for the host to queue every launch of the call (torch.cuda._sleep,
+    # calibrated to ~150 µs), HIP events right around the call; the host-paced time
+    # (no spin: each launch waits for its ctypes / RCCL enqueue) is reported beside it.
+    spin = None
+    if hasattr(torch.cuda, "_sleep"):
+        a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a0.record()
+        torch.cuda._sleep(1_000_000)
+        b0.record()
+        torch.cuda.synchronize()
+        spin = max(1, int(1_000_000 * 0.15 / max(a0.elapsed_time(b0), 1e-3)))
+
+    def window(fn, pre_spin):
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
-        plan.timer_enable(4 * iters)
         for a, b in evs:
+            if pre_spin:
+                torch.cuda._sleep(spin)
             a.record()
             fn()
             b.record()
         torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in evs) / iters
+
+    rows = {}
+    for name, fn in (("clip_path_zero_n8", folded), ("clip_path_zero_n8_scalar", scalar)):
+        for _ in range(3):
+            fn()
+        host_ms = window(fn, False)
+        ms = window(fn, True) if spin else host_ms
+        plan.timer_enable(4 * iters)  # the kernels alone (plan launch timer), a separate pass
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
         kern = plan.timer_read()
         plan.timer_enable(0)
-        ms = sum(a.elapsed_time(b) for a, b in evs) / iters
         nbytes = 30 * shard
         rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9,
                       "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "shard_elems": shard,
-                      "kernels_ms": sum(kern) / iters,
+                      "kernels_ms": sum(kern) / iters, "host_paced_ms": host_ms,
+                      "timing": ("HIP events around the call, the stream pre-loaded by a spin kernel (the launches "
+                                 "queued ahead, as behind backward)" if spin else "HIP events around the call"),
                       "launches": ("sqnorm_partial_out + all_reduce(<=64 floats) + clipped AdamW"
                                    if name == "clip_path_zero_n8" else
                                    "sqnorm (in-kernel combine) + all_reduce(scalar) + clipped AdamW")}

