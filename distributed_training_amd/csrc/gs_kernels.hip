@@ -104,14 +104,24 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #ifndef GS_NT_LOAD
 #define GS_NT_LOAD 0
 #endif
-// non-temporal loads for the updates' read-once gradient stream only
+// Non-temporal loads in the fused updates (profiles/r4/r4c_nt_instep.jsonl,
+// r4e_nt_state.jsonl: bench.py in the training step + the beyond-Infinity-Cache
+// rows, library variants interleaved, two rounds):
+// * the read-once gradient stream: always (in-step ResNet-50 SGD 0.786 -> 0.805-0.816
+//   of 8 TB/s; back-to-back ResNet-152 x 2 SGD 0.709 -> 0.729);
+// * the parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq): never
+//   by default.  Back to back beyond the cache NT loads there lift SGD to 0.76, but
+//   in the training step they cost every configuration measured — ResNet-50 SGD
+//   0.79 -> 0.70, ResNet-50 Adam 0.82 -> 0.73, ResNet-152 SGD (481 MB of state, far
+//   beyond the cache) 0.83 -> 0.74.  GS_NT_STATE (env) = 1 forces them, 2 = only
+//   when p + the fp32 states exceed the 256 MiB cache (the A/B rule measured above).
 #ifndef GS_NT_LOAD_GRAD
-#define GS_NT_LOAD_GRAD GS_NT_LOAD
+#define GS_NT_LOAD_GRAD 1
 #endif
-// ... and for their parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq)
-#ifndef GS_NT_LOAD_STATE
-#define GS_NT_LOAD_STATE GS_NT_LOAD
+#ifndef GS_NT_STATE_DEFAULT
+#define GS_NT_STATE_DEFAULT 0
 #endif
+constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 #ifndef GS_NT_STORE
 #define GS_NT_STORE 1
 #endif
@@ -1069,7 +1079,8 @@ struct UnscaleOp {
 };
 
 // SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
-template <int N, int GD, int LD>
+// NTS: non-temporal loads of p and the momentum buffer (the state streams, above)
+template <int N, int GD, int LD, bool NTS = false>
 struct SgdOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_SGD;
@@ -1093,9 +1104,9 @@ struct SgdOp {
   }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
     ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
-    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1121,7 +1132,7 @@ struct SgdOp {
 };
 
 // Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
-template <int N, int GD, int LD>
+template <int N, int GD, int LD, bool NTS = false>
 struct AdamOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_ADAM;
@@ -1145,10 +1156,10 @@ struct AdamOp {
   }
   template <bool F>
   __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
     ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
-    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
-    ld<GS_F32, N, F, GS_NT_LOAD_STATE != 0>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+    ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }
   template <bool F>
   __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1210,16 +1221,16 @@ __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
 }
-template <int N, int GD, int LD>
-__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD>& op) {
+template <int N, int GD, int LD, bool NTS>
+__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTS>& op) {
   if (op.hyper) {
     op.h.lr = op.hyper[0];
     if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
   }
   load_grad_multiplier(op);
 }
-template <int N, int GD, int LD>
-__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD>& op) {
+template <int N, int GD, int LD, bool NTS>
+__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTS>& op) {
   if (op.hyper) {
     op.h.step_size = op.hyper[0];
     op.h.bc2s = op.hyper[1];
@@ -1690,11 +1701,43 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
   return GS_OK;
 }
 
+// non-temporal loads of the update's state streams (GS_NT_STATE, above): never,
+// always, or when p + the fp32 states (state_streams of them) exceed 256 MiB
+bool nt_state(const gs_plan* p, int state_streams) {
+  static const int policy = [] {
+    const char* e = std::getenv("GS_NT_STATE");
+    return e ? std::atoi(e) : GS_NT_STATE_DEFAULT;
+  }();
+  if (policy != 2) return policy != 0;
+  int64_t n = 0;
+  for (int64_t x : p->numel) n += x;
+  return n * 4 * (1 + state_streams) > kInfinityCacheBytes;
+}
+
+template <bool NTS>
+static int sgd_nts(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
+                   const ClipArgs* clip, void* stream) {
+  GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
+    SgdOp<GS_OPT_N, GD, LD, NTS> op;
+    op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
+    if (clip) { op.clip = *clip; op.clip_on = true; }
+    return launch<GS_OPT_ILP>(p, op, stream);
+  }));
+  return GS_OK;
+}
+
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
             const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
+  if (nt_state(p, h.mom != 0.f ? 1 : 0)) return sgd_nts<true>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  return sgd_nts<false>(p, gdt, ldt, h, gsc, fi, clip, stream);
+}
+
+template <bool NTS>
+static int adam_nts(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
+                    const ClipArgs* clip, void* stream) {
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    SgdOp<GS_OPT_N, GD, LD> op;
+    AdamOp<GS_OPT_N, GD, LD, NTS> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
     if (clip) { op.clip = *clip; op.clip_on = true; }
     return launch<GS_OPT_ILP>(p, op, stream);
@@ -1705,13 +1748,8 @@ int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, c
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
              const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    AdamOp<GS_OPT_N, GD, LD> op;
-    op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
-    if (clip) { op.clip = *clip; op.clip_on = true; }
-    return launch<GS_OPT_ILP>(p, op, stream);
-  }));
-  return GS_OK;
+  if (nt_state(p, 2)) return adam_nts<true>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  return adam_nts<false>(p, gdt, ldt, h, gsc, fi, clip, stream);
 }
 
 }  // namespace gs
