@@ -107,8 +107,10 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 // Non-temporal loads in the fused updates (profiles/r4/r4c_nt_instep.jsonl,
 // r4e_nt_state.jsonl: bench.py in the training step + the beyond-Infinity-Cache
 // rows, library variants interleaved, two rounds):
-// * the read-once gradient stream: always (in-step ResNet-50 SGD 0.786 -> 0.805-0.816
-//   of 8 TB/s; back-to-back ResNet-152 x 2 SGD 0.709 -> 0.729);
+// * the read-once gradient stream: unless a folded clip's Σg² pass read it just before
+//   (in-step ResNet-50 SGD 0.786 -> 0.805-0.816 of 8 TB/s; back-to-back ResNet-152 x 2
+//   SGD 0.709 -> 0.729; but the clip path's update, right behind the Σg² kernel that
+//   brought the grads into the caches, 0.770 -> 0.740 with NT grad loads);
 // * the parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq): never
 //   by default.  Back to back beyond the cache NT loads there lift SGD to 0.76, but
 //   in the training step they cost every configuration measured — ResNet-50 SGD
@@ -1079,8 +1081,8 @@ struct UnscaleOp {
 };
 
 // SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
-// NTS: non-temporal loads of p and the momentum buffer (the state streams, above)
-template <int N, int GD, int LD, bool NTS = false>
+// NTG / NTS: non-temporal loads of the grad / of p and the momentum buffer (above)
+template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
 struct SgdOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_SGD;
@@ -1105,7 +1107,7 @@ struct SgdOp {
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
     ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
-    ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
+    ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
     if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
   template <bool F>
@@ -1132,7 +1134,7 @@ struct SgdOp {
 };
 
 // Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
-template <int N, int GD, int LD, bool NTS = false>
+template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
 struct AdamOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_ADAM;
@@ -1157,7 +1159,7 @@ struct AdamOp {
   template <bool F>
   __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
     ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
-    ld<GD, N, F, GS_NT_LOAD_GRAD != 0>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
+    ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
     ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
     ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }
@@ -1221,16 +1223,16 @@ __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
 }
-template <int N, int GD, int LD, bool NTS>
-__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTS>& op) {
+template <int N, int GD, int LD, bool NTG, bool NTS>
+__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTG, NTS>& op) {
   if (op.hyper) {
     op.h.lr = op.hyper[0];
     if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
   }
   load_grad_multiplier(op);
 }
-template <int N, int GD, int LD, bool NTS>
-__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTS>& op) {
+template <int N, int GD, int LD, bool NTG, bool NTS>
+__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTG, NTS>& op) {
   if (op.hyper) {
     op.h.step_size = op.hyper[0];
     op.h.bc2s = op.hyper[1];
@@ -1714,11 +1716,14 @@ bool nt_state(const gs_plan* p, int state_streams) {
   return n * 4 * (1 + state_streams) > kInfinityCacheBytes;
 }
 
-template <bool NTS>
-static int sgd_nts(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
-                   const ClipArgs* clip, void* stream) {
+// grads read just before by a folded clip's Σg² kernel stay in the caches: cached loads
+bool nt_grad(const ClipArgs* clip) { return GS_NT_LOAD_GRAD != 0 && clip == nullptr; }
+
+template <bool NTG, bool NTS>
+static int sgd_nt(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
+                  const ClipArgs* clip, void* stream) {
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    SgdOp<GS_OPT_N, GD, LD, NTS> op;
+    SgdOp<GS_OPT_N, GD, LD, NTG, NTS> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
     if (clip) { op.clip = *clip; op.clip_on = true; }
     return launch<GS_OPT_ILP>(p, op, stream);
@@ -1729,15 +1734,18 @@ static int sgd_nts(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float*
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
             const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  if (nt_state(p, h.mom != 0.f ? 1 : 0)) return sgd_nts<true>(p, gdt, ldt, h, gsc, fi, clip, stream);
-  return sgd_nts<false>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  const bool ntg = nt_grad(clip), nts = nt_state(p, h.mom != 0.f ? 1 : 0);
+  if (ntg) return nts ? sgd_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
+                      : sgd_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  return nts ? sgd_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
+             : sgd_nt<false, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
 }
 
-template <bool NTS>
-static int adam_nts(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
-                    const ClipArgs* clip, void* stream) {
+template <bool NTG, bool NTS>
+static int adam_nt(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
+                   const ClipArgs* clip, void* stream) {
   GS_DISPATCH_FLOAT(gdt, GD, GS_DISPATCH_LOWP(ldt, LD, {
-    AdamOp<GS_OPT_N, GD, LD, NTS> op;
+    AdamOp<GS_OPT_N, GD, LD, NTG, NTS> op;
     op.h = h; op.gscale = gsc; op.found_inf = fi; op.hyper = p->hyper;
     if (clip) { op.clip = *clip; op.clip_on = true; }
     return launch<GS_OPT_ILP>(p, op, stream);
@@ -1748,8 +1756,11 @@ static int adam_nts(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const floa
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
              const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  if (nt_state(p, 2)) return adam_nts<true>(p, gdt, ldt, h, gsc, fi, clip, stream);
-  return adam_nts<false>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  const bool ntg = nt_grad(clip), nts = nt_state(p, 2);
+  if (ntg) return nts ? adam_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
+                      : adam_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
+  return nts ? adam_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
+             : adam_nt<false, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
 }
 
 }  // namespace gs
