@@ -456,10 +456,11 @@ def _engine_comm(ddp, zero):
 # Cost estimates of the optional legs after the timed region (seconds), for the
 # --wall-budget-s skip decision: the larger of the N=1 run with every leg forced on
 # (profiles/r3/r3n_bench_n1_all_legs.json leg_seconds) and the 4-rank full-size
-# rehearsal (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json), doubled,
+# rehearsals (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json,
+# profiles/r4/r4d_n4_budget240.json), doubled,
 # and at least 5 s; zero2 / colossal include their first-step MIOpen compiles.
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
-              "zero2": 2 * 8.4, "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 16.2}
+              "zero2": 2 * 18.4, "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 35.0}
 # the reference's DeepSpeed optimizer (R:resnet/deepspeed/deepspeed_train.py:175-186): "Adam" in
 # AdamW mode, betas (0.8, 0.999), eps 1e-8, weight_decay 3e-7; gradient_clipping 1.0 (:195)
 DS_ADAM = dict(lr=1e-3, betas=(0.8, 0.999), eps=1e-8, weight_decay=3e-7)

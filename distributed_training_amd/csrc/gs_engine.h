@@ -1,0 +1,1358 @@
+// The gfx950 streaming engine of libgsync, shared by the kernel translation units
+// (gs_kernels.hip: pack / unpack / reductions / plan memory; gs_update_kernels.hip:
+// the fused SGD / Adam updates — two TUs so hipcc compiles them in parallel).
+// Device code: include from .hip sources only.
+//
+// All of them are HBM-streaming kernels (no MFMA: nothing here is a
+// contraction).  One work decomposition serves every op: a plan cuts each
+// tensor into 4-element units, units into segments (<= 16 Ki elements) and
+// segments into tasks (<= 16 Ki elements, <= 64 segments).  A 256-thread
+// workgroup (4 wave64) takes one task at a time; the task's segment
+// descriptors are staged in LDS so that a workgroup gathers many small
+// tensors (BN weights/biases, 1x1-conv biases ...) in one pass with every
+// lane busy, while a large tensor gets one segment per task.  Every lane
+// moves 4 elements per access (16 B for fp32, 8 B for bf16/fp16) with ILP
+// accesses in flight before the first use.
+//
+// Arithmetic is written with explicit fmaf and compiled with
+// -ffp-contract=off so that the host restatement (oracle/gs_oracle.c) and
+// the host backend (gs_host.cpp) reproduce it bit for bit.
+
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "gs_common.h"
+
+namespace gs {
+
+namespace {
+
+#define HIP_RET(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(GS_EHIP, std::string(#expr " failed: ") + hipGetErrorString(_e));   \
+  } while (0)
+
+// ---------------------------------------------------------------- dtype I/O
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+// round-to-nearest-even; NaN -> 0x7FC0 (c10::BFloat16 round_to_nearest_even)
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7FC0;
+  return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  _Float16 x;
+  __builtin_memcpy(&x, &h, 2);
+  return static_cast<float>(x);
+}
+// fp32 -> fp16, round-to-nearest-even of the fp32 VALUE (torch: opmath in fp32,
+// then the cast).  The empty asm pins f as an fp32 register value: without it
+// LLVM folds the producing fma / mul into v_fma_mixlo_f16, which rounds the
+// exact result once, straight to fp16 — a different fp16 wherever the fp32
+// rounding lands on an fp16 tie (ZeRO fp16 params, fp16 buckets, fp16 unscale;
+// found as master.half() != the fp16 param in test_colossal_low_level_zero_fp16_gpu)
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  __asm__("" : "+v"(f));
+  _Float16 x = static_cast<_Float16>(f);
+  uint16_t h;
+  __builtin_memcpy(&h, &x, 2);
+  return h;
+}
+
+template <int DT>
+__device__ __forceinline__ float to_f32(uint16_t h) {
+  if constexpr (DT == GS_BF16) return bf16_to_f32(h);
+  else return f16_to_f32(h);
+}
+template <int DT>
+__device__ __forceinline__ uint16_t from_f32(float f) {
+  if constexpr (DT == GS_BF16) return f32_to_bf16(f);
+  else return f32_to_f16(f);
+}
+// value as it would read back after a store in DT (used for norms / casts)
+template <int DT>
+__device__ __forceinline__ float round_to(float f) {
+  if constexpr (DT == GS_F32) return f;
+  else return to_f32<DT>(from_f32<DT>(f));
+}
+
+// Plan pointers are read from a table, so the compiler only sees generic
+// pointers and would emit flat_* accesses; every buffer here is device
+// global memory, so accesses go through address_space(1) (global_*) with
+// native 16-B / 8-B vector types.
+typedef float gf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t gu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t gu4 __attribute__((ext_vector_type(4)));
+#define GLOBAL_AS __attribute__((address_space(1)))
+
+template <class T>
+__device__ __forceinline__ const GLOBAL_AS T* gptr(const void* p) {
+  return (const GLOBAL_AS T*)(p);
+}
+template <class T>
+__device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
+  return (GLOBAL_AS T*)(p);
+}
+
+// Build-time tuning knobs (defaults are the measured best)
+#ifndef GS_NT_LOAD
+#define GS_NT_LOAD 0
+#endif
+// Non-temporal loads in the fused updates (profiles/r4/r4c_nt_instep.jsonl,
+// r4e_nt_state.jsonl: bench.py in the training step + the beyond-Infinity-Cache
+// rows, library variants interleaved, two rounds):
+// * the read-once gradient stream: unless a folded clip's Σg² pass read it just before
+//   (in-step ResNet-50 SGD 0.786 -> 0.805-0.816 of 8 TB/s; back-to-back ResNet-152 x 2
+//   SGD 0.709 -> 0.729; but the clip path's update, right behind the Σg² kernel that
+//   brought the grads into the caches, 0.770 -> 0.740 with NT grad loads);
+// * the parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq): never
+//   by default.  Back to back beyond the cache NT loads there lift SGD to 0.76, but
+//   in the training step they cost every configuration measured — ResNet-50 SGD
+//   0.79 -> 0.70, ResNet-50 Adam 0.82 -> 0.73, ResNet-152 SGD (481 MB of state, far
+//   beyond the cache) 0.83 -> 0.74.  GS_NT_STATE (env) = 1 forces them, 2 = only
+//   when p + the fp32 states exceed the 256 MiB cache (the A/B rule measured above).
+#ifndef GS_NT_LOAD_GRAD
+#define GS_NT_LOAD_GRAD 1
+#endif
+#ifndef GS_NT_STATE_DEFAULT
+#define GS_NT_STATE_DEFAULT 0
+#endif
+constexpr int64_t kInfinityCacheBytes = 256ll << 20;
+#ifndef GS_NT_STORE
+#define GS_NT_STORE 1
+#endif
+#ifndef GS_PACK_ILP
+#define GS_PACK_ILP 4
+#endif
+#ifndef GS_OPT_ILP
+#define GS_OPT_ILP 2
+#endif
+// read-only reductions (Σg²) keep more loads in flight per lane
+#ifndef GS_RED_ILP
+#define GS_RED_ILP 4
+#endif
+// elements per lane-step (4 or 8): 8 gives 16-B accesses to 16-bit streams
+#ifndef GS_PACK_N
+#define GS_PACK_N 4
+#endif
+#ifndef GS_OPT_N
+#define GS_OPT_N 4
+#endif
+// chunks per workgroup iteration (chunk-map engine), per op; measured in
+// profiles/r2*_kernels_*.jsonl (scripts/r2_engine_ab.sh)
+// in-kernel combine of capped chunk-engine reductions (two-level ticket over
+// GS_RED_FUSE groups) instead of the combine_partials launch (0); the
+// environment variable of the same name overrides.
+// A single-counter ticket measured slower than the launch (r2c).
+#ifndef GS_RED_FUSE
+#define GS_RED_FUSE 64
+#endif
+#ifndef GS_RED_FUSE_GRID
+#define GS_RED_FUSE_GRID 2048  // workgroups of a fused reduction (r2z2 sweep: 2048 < 4096 < 8192)
+#endif
+constexpr int kRedSyncWords = (2 * kRedMaxGroups + 1) * kRedSyncStride;
+constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too many arrivals
+#ifndef GS_G_PACK
+#define GS_G_PACK 1     // fp32 bucket
+#endif
+#ifndef GS_G_PACK16
+#define GS_G_PACK16 8   // 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
+#endif
+#ifndef GS_G_UNPACK
+#define GS_G_UNPACK 2
+#endif
+#ifndef GS_G_RED
+#define GS_G_RED 2
+#endif
+#ifndef GS_G_SGD
+#define GS_G_SGD 2
+#endif
+#ifndef GS_G_ADAM
+#define GS_G_ADAM 4
+#endif
+// 256-thread workgroups are admitted 8 per CU only while the kernel uses <= 80
+// SGPRs (MI355X_MICROARCH.md, residency); cap the allocation there
+#ifndef GS_NUM_SGPR
+#define GS_NUM_SGPR 80
+#endif
+#if GS_NUM_SGPR > 0
+#define GS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GS_NUM_SGPR)))
+#else
+#define GS_SGPR_ATTR
+#endif
+
+template <bool NT = (GS_NT_LOAD != 0), class V>
+__device__ __forceinline__ V vload(const GLOBAL_AS V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <class V>
+__device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
+#if GS_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// load N (4 or 8) consecutive elements [e, e+N) of a tensor with n elements;
+// e is a multiple of N.  fp32: N/4 16-B loads; 16-bit: one 8-B (N=4) or
+// 16-B (N=8) load.  `vec`: the tensor base is 16-B aligned.
+template <int DT, int N, bool NT = (GS_NT_LOAD != 0)>
+__device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bool vec,
+                                      float (&x)[N]) {
+  static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
+  if constexpr (DT == GS_F32) {
+    const GLOBAL_AS float* p = gptr<float>(base) + e;
+    if (vec && e + N <= n) {
+#pragma unroll
+      for (int h = 0; h < N / 4; ++h) {
+        const gf4 v = vload<NT>((const GLOBAL_AS gf4*)(p + 4 * h));
+        x[4 * h + 0] = v.x; x[4 * h + 1] = v.y; x[4 * h + 2] = v.z; x[4 * h + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) x[i] = (e + i < n) ? p[i] : 0.f;
+    }
+  } else {
+    const GLOBAL_AS uint16_t* p = gptr<uint16_t>(base) + e;
+    if (vec && e + N <= n) {
+      uint32_t w[N / 2];
+      if constexpr (N == 8) {
+        const gu4 v = vload<NT>((const GLOBAL_AS gu4*)p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      } else {
+        const gu2 v = vload<NT>((const GLOBAL_AS gu2*)p);
+        w[0] = v.x; w[1] = v.y;
+      }
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k) {
+        x[2 * k] = to_f32<DT>(static_cast<uint16_t>(w[k] & 0xffffu));
+        x[2 * k + 1] = to_f32<DT>(static_cast<uint16_t>(w[k] >> 16));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) x[i] = (e + i < n) ? to_f32<DT>(p[i]) : 0.f;
+    }
+  }
+}
+
+template <int DT, int N>
+__device__ __forceinline__ void storeN(void* base, int64_t e, int64_t n, bool vec,
+                                       const float (&x)[N]) {
+  static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
+  if constexpr (DT == GS_F32) {
+    GLOBAL_AS float* p = gptr_w<float>(base) + e;
+    if (vec && e + N <= n) {
+#pragma unroll
+      for (int h = 0; h < N / 4; ++h) {
+        gf4 v;
+        v.x = x[4 * h + 0]; v.y = x[4 * h + 1]; v.z = x[4 * h + 2]; v.w = x[4 * h + 3];
+        vstore((GLOBAL_AS gf4*)(p + 4 * h), v);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (e + i < n) p[i] = x[i];
+    }
+  } else {
+    GLOBAL_AS uint16_t* p = gptr_w<uint16_t>(base) + e;
+    if (vec && e + N <= n) {
+      uint32_t w[N / 2];
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k)
+        w[k] = static_cast<uint32_t>(from_f32<DT>(x[2 * k])) |
+               (static_cast<uint32_t>(from_f32<DT>(x[2 * k + 1])) << 16);
+      if constexpr (N == 8) {
+        gu4 v;
+        v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+        vstore((GLOBAL_AS gu4*)p, v);
+      } else {
+        gu2 v;
+        v.x = w[0]; v.y = w[1];
+        vstore((GLOBAL_AS gu2*)p, v);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (e + i < n) p[i] = from_f32<DT>(x[i]);
+    }
+  }
+}
+
+// Full-chunk access of the chunk-map engine: `base` is wave-uniform (SGPRs),
+// e0 the uniform element index of the chunk inside the tensor and `lo` the
+// lane's 32-bit element offset; everything is in range and 16-B aligned, so
+// the access is one global_load/store with an SGPR base and a VGPR offset.
+template <int DT>
+__device__ __forceinline__ const void* elem_at(const void* base, int64_t e0) {
+  return static_cast<const char*>(base) + e0 * (DT == GS_F32 ? 4 : 2);
+}
+template <int DT, bool NT = (GS_NT_LOAD != 0)>
+__device__ __forceinline__ void load4F(const void* base, uint32_t lo, float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    const gf4 v = vload<NT>((const GLOBAL_AS gf4*)(gptr<float>(base) + lo));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+    const gu2 v = vload<NT>((const GLOBAL_AS gu2*)(gptr<uint16_t>(base) + lo));
+    x[0] = to_f32<DT>(static_cast<uint16_t>(v.x & 0xffffu));
+    x[1] = to_f32<DT>(static_cast<uint16_t>(v.x >> 16));
+    x[2] = to_f32<DT>(static_cast<uint16_t>(v.y & 0xffffu));
+    x[3] = to_f32<DT>(static_cast<uint16_t>(v.y >> 16));
+  }
+}
+template <int DT>
+__device__ __forceinline__ void store4F(void* base, uint32_t lo, const float (&x)[4]) {
+  if constexpr (DT == GS_F32) {
+    gf4 v;
+    v.x = x[0]; v.y = x[1]; v.z = x[2]; v.w = x[3];
+    vstore((GLOBAL_AS gf4*)(gptr_w<float>(base) + lo), v);
+  } else {
+    gu2 v;
+    v.x = static_cast<uint32_t>(from_f32<DT>(x[0])) | (static_cast<uint32_t>(from_f32<DT>(x[1])) << 16);
+    v.y = static_cast<uint32_t>(from_f32<DT>(x[2])) | (static_cast<uint32_t>(from_f32<DT>(x[3])) << 16);
+    vstore((GLOBAL_AS gu2*)(gptr_w<uint16_t>(base) + lo), v);
+  }
+}
+// F = full-chunk fast path (above); otherwise element e0 + lo of a tensor of
+// n elements with the bounds / alignment checks of loadN / storeN
+template <int DT, int N, bool F, bool NT = (GS_NT_LOAD != 0)>
+__device__ __forceinline__ void ld(const void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
+                                   float (&x)[N]) {
+  if constexpr (F) {
+    static_assert(N == 4, "the chunk engine moves 4 elements per lane-access");
+    load4F<DT, NT>(elem_at<DT>(base, e0), lo, x);
+  } else {
+    loadN<DT, N, NT>(base, e0 + lo, n, vec, x);
+  }
+}
+template <int DT, int N, bool F>
+__device__ __forceinline__ void st(void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
+                                   const float (&x)[N]) {
+  if constexpr (F) {
+    static_assert(N == 4, "the chunk engine moves 4 elements per lane-access");
+    store4F<DT>(const_cast<void*>(elem_at<DT>(base, e0)), lo, x);
+  } else {
+    storeN<DT, N>(base, e0 + lo, n, vec, x);
+  }
+}
+
+__device__ __forceinline__ void* slot_ptr(const PlanArgs& P, int slot, int t) {
+  return P.ptrs[static_cast<int64_t>(slot) * P.n + t];
+}
+__device__ __forceinline__ bool slot_vec(const PlanArgs& P, int slot, int t) {
+  return (P.align[t] >> slot) & 1u;
+}
+
+// ------------------------------------------------------- wave/block reduce
+// DPP wave reduction (GFX9 DPP, all in VALU — no LDS crossbar): quad swaps,
+// half-row and row mirrors give every lane its row-of-16 total, row_bcast:15
+// folds rows 0->1 and 2->3, row_bcast:31 folds row 1 into rows 2-3, so lane
+// 63 holds the wave total; v_readlane broadcasts it.  A fixed tree:
+// deterministic.  Lanes of rows a DPP op does not write keep `id`.
+template <int Ctrl, int RowMask, bool MAX>
+__device__ __forceinline__ float dpp_op(float v, float id) {
+  const int s = __builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), Ctrl, RowMask, 0xF, false);
+  const float t = __int_as_float(s);
+  return MAX ? fmaxf(v, t) : v + t;
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce(float v) {
+  const float id = MAX ? -INFINITY : 0.f;
+  v = dpp_op<0xB1, 0xF, MAX>(v, id);   // quad_perm [1,0,3,2]
+  v = dpp_op<0x4E, 0xF, MAX>(v, id);   // quad_perm [2,3,0,1]
+  v = dpp_op<0x141, 0xF, MAX>(v, id);  // row_half_mirror
+  v = dpp_op<0x140, 0xF, MAX>(v, id);  // row_mirror
+  v = dpp_op<0x142, 0xA, MAX>(v, id);  // row_bcast:15 into rows 1, 3
+  v = dpp_op<0x143, 0xC, MAX>(v, id);  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_sum(float v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v); }
+// block of kBlock threads; result valid in thread 0
+template <bool MAX>
+__device__ __forceinline__ float block_reduce(float v) {
+  __shared__ float s_red[kBlock / 64];
+  v = MAX ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) s_red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0) {
+    r = s_red[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; ++i) r = MAX ? fmaxf(r, s_red[i]) : r + s_red[i];
+  }
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------- the engine
+// Everything a unit needs about its tensor, staged once per task in LDS
+// (one entry per segment of the task) instead of re-read from the global
+// tables for every unit.
+struct TV {
+  void* ptr[GS_PLAN_SLOTS];
+  int64_t numel;
+  int64_t off;
+  uint32_t align;
+  int32_t pad;
+  __device__ __forceinline__ bool vec(int slot) const { return (align >> slot) & 1u; }
+};
+
+// Op contract:
+//   struct Frag;                             registers for one unit (4 elements)
+//   load_hyper(Op&) overload (optional)      step-varying hyper-parameters from device memory
+//   bool active() const;                     uniform early-out (found_inf skip)
+//   void load(const TV&, e, Frag&)           issue the unit's loads
+//   void apply(const TV&, e, Frag&, acc)     compute + store (+ reduction)
+//   static constexpr int kRed = 0 (none) | 1 (sum) | 2 (max); float* partials
+//   static constexpr int kKind = GS_OP_* (tags the launch timer's records)
+// default: hyper-parameters travel in the kernel arguments
+template <class Op>
+__device__ __forceinline__ void load_hyper(Op&) {}
+
+template <int ILP, class Op>
+__device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
+                                          const int32_t* s_pref, int ns, int total, float& acc) {
+  // a lane-step covers U consecutive units (U = Op::kN / 4); segments hold an
+  // even number of units (the plan pads), so a step never straddles two
+  constexpr int U = Op::kN / kUnit;
+  if (ns == 1) {
+    // one (large) tensor segment: descriptor in registers, no per-unit search
+    const TV v = s_tv[0];
+    const int64_t ub = s_ubeg[0];
+    for (int base = 0; base < total; base += kBlock * ILP * U) {
+      typename Op::Frag f[ILP];
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+        if (u < total) op.template load<false>(v, (ub + u) * kUnit, 0u, f[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) {
+        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+        if (u < total) op.template apply<false>(v, (ub + u) * kUnit, 0u, f[j], acc);
+      }
+    }
+    return;
+  }
+  // many small tensors share the task: binary search in the LDS prefix
+  for (int base = 0; base < total; base += kBlock * ILP * U) {
+    typename Op::Frag f[ILP];
+    int kk[ILP];
+    int64_t ee[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+      kk[j] = -1;
+      if (u < total) {
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_pref[mid] <= u) lo = mid; else hi = mid - 1;
+        }
+        kk[j] = lo;
+        ee[j] = (s_ubeg[lo] + (u - s_pref[lo])) * kUnit;
+        op.template load<false>(s_tv[lo], ee[j], 0u, f[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j)
+      if (kk[j] >= 0) op.template apply<false>(s_tv[kk[j]], ee[j], 0u, f[j], acc);
+  }
+}
+
+// part `part` of `parts` of one tensor of `total` units: lane-step chunks of
+// C = kBlock * ILP * U units, chunk c taken by part c % parts
+template <int ILP, class Op>
+__device__ __forceinline__ void run_interleaved(const Op& op, const TV& v, int part, int parts, int total,
+                                                float& acc) {
+  constexpr int U = Op::kN / kUnit;
+  constexpr int C = kBlock * ILP * U;
+  for (int base = part * C; base < total; base += parts * C) {
+    typename Op::Frag f[ILP];
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+      if (u < total) op.template load<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < ILP; ++j) {
+      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
+      if (u < total) op.template apply<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j], acc);
+    }
+  }
+}
+
+// The plan tables are read-only for the whole launch: reading them through
+// the constant address space lets the uniform descriptor loads of a
+// single-segment task go to the scalar unit (s_load), with no LDS round trip
+// and no barrier before the first data load.
+#define CONST_AS __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ T cload(const T* p, int64_t i) {
+  return ((const CONST_AS T*)(p))[i];
+}
+
+// Descriptor of tensor t as `op` addresses it: logical slot k is table row
+// op.phys(k), so single-stream ops read their runtime slot as the constant
+// logical slot 0.  (A runtime index into TV::ptr made the compiler spill the
+// descriptor to scratch and reload the stream pointer into VGPRs, turning
+// every access into per-lane 64-bit addressing.)  SCALAR: wave-uniform t,
+// loaded through the constant address space (s_load).
+template <bool SCALAR, class Op>
+__device__ __forceinline__ TV load_tv(const Op& op, const PlanArgs& P, int t) {
+  TV v;
+  const uint32_t a = SCALAR ? cload(P.align, t) : P.align[t];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int s = 0; s < GS_PLAN_SLOTS; ++s) {
+    const int64_t r = static_cast<int64_t>(op.phys(s)) * P.n + t;
+    v.ptr[s] = SCALAR ? cload(P.ptrs, r) : P.ptrs[r];
+    bits |= ((a >> op.phys(s)) & 1u) << s;
+  }
+  v.align = bits;
+  v.numel = SCALAR ? cload(P.numel, t) : P.numel[t];
+  v.off = SCALAR ? cload(P.off, t) : P.off[t];
+  v.pad = 0;
+  return v;
+}
+
+template <int ILP, class Op>
+__global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op op) {
+  __shared__ TV s_tv[kMaxSegPerTask];
+  __shared__ int64_t s_ubeg[kMaxSegPerTask];
+  __shared__ int32_t s_pref[kMaxSegPerTask + 1];
+  float acc = 0.f;
+  load_hyper(op);             // uniform: graph-replayable lr / bias corrections, clip coefficient
+  if (!op.active()) return;  // uniform across the grid
+  for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
+    const int sb = cload(P.task_begin, task);
+    const int ns = cload(P.task_begin, task + 1) - sb;
+    if (ns == 1) {
+      // one (large) tensor segment: wave-uniform descriptor in SGPRs
+      const CONST_AS Seg* q = ((const CONST_AS Seg*)(P.segs)) + sb;
+      const int t = q->tensor;
+      const int64_t ub = q->unit_begin;
+      const int units = q->units;
+      const int parts = q->pad;
+      const TV v = load_tv<true>(op, P, t);
+      if (parts > 0) run_interleaved<ILP>(op, v, static_cast<int>(ub), parts, units, acc);
+      else run_units<ILP>(op, &v, &ub, nullptr, 1, units, acc);
+      continue;
+    }
+    if (threadIdx.x < ns) {
+      const Seg sg = P.segs[sb + threadIdx.x];
+      const int t = sg.tensor;
+      s_tv[threadIdx.x] = load_tv<false>(op, P, t);
+      s_ubeg[threadIdx.x] = sg.unit_begin;
+      s_pref[threadIdx.x] = sg.task_off;
+      if (threadIdx.x == ns - 1) s_pref[ns] = sg.task_off + sg.units;
+    }
+    __syncthreads();
+    run_units<ILP>(op, s_tv, s_ubeg, s_pref, ns, s_pref[ns], acc);
+    __syncthreads();
+  }
+  if constexpr (Op::kRed != 0) {
+    const float r = block_reduce<Op::kRed == 2>(acc);
+    if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+  }
+}
+
+// deterministic combine of the per-workgroup partials (fixed order): 1024
+// threads, thread t folds the float4s t, t+1024, ... (8 16-B loads issued
+// before the first add: up to 32 Ki partials — the uncapped unpack + Σg² grid
+// of a ResNet-50 — in one round trip), the < 4 trailing partials go to threads
+// 0-2, then a fixed-tree block reduction
+constexpr int kCombineBlock = 1024;
+template <bool MAX>
+__global__ void __launch_bounds__(kCombineBlock) combine_partials(const float* partials, int n,
+                                                                  float* out, int accumulate) {
+  __shared__ float s_red[kCombineBlock / 64];
+  float v = 0.f;
+  const int n4 = n >> 2;
+  const float4* p4 = reinterpret_cast<const float4*>(partials);  // hipMalloc'd: 16-B aligned
+  for (int i = threadIdx.x; i < n4; i += 8 * kCombineBlock) {
+    float4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      x[u] = (i + u * kCombineBlock < n4) ? p4[i + u * kCombineBlock] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (i + u * kCombineBlock < n4) {
+        v = MAX ? fmaxf(v, x[u].x) : v + x[u].x;
+        v = MAX ? fmaxf(v, x[u].y) : v + x[u].y;
+        v = MAX ? fmaxf(v, x[u].z) : v + x[u].z;
+        v = MAX ? fmaxf(v, x[u].w) : v + x[u].w;
+      }
+    }
+  }
+  if (static_cast<int>(threadIdx.x) < (n & 3)) {
+    const float x = partials[4 * n4 + threadIdx.x];
+    v = MAX ? fmaxf(v, x) : v + x;
+  }
+  v = MAX ? wave_max(v) : wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kCombineBlock / 64; ++w) r = MAX ? fmaxf(r, s_red[w]) : r + s_red[w];
+    if (MAX) out[0] = accumulate ? fmaxf(out[0], r) : r;
+    else out[0] = accumulate ? out[0] + r : r;
+  }
+}
+
+// ------------------------------------------------------- chunk-map engine
+// (layout: gs_common.h).  A workgroup takes G consecutive 1 Ki-element chunks
+// per iteration and grid-strides.  A group wholly inside one tensor whose
+// streams are all 16-B aligned runs the op's F = true path: the descriptor
+// comes through scalar loads and every lane issues G 16-B accesses per stream
+// (SGPR base + 32-bit VGPR offset) before the first use, with no bounds or
+// alignment branches.  Other groups go chunk by chunk: a full chunk the same
+// way with one access per lane, a mixed chunk (tensor tails, runs of small
+// tensors) by a per-lane binary search over voff and the checked path.
+// Reductions write one partial per workgroup; the grid is capped for them so
+// that the combine reads few partials (combine_partials, fixed order).
+template <class Op>
+__device__ __forceinline__ void chunk_mixed(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
+                                            float& acc) {
+  const int64_t e = c * kChunkElems + static_cast<int>(threadIdx.x) * kUnit;
+  int lo = t0, hi = t0 + span - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P.voff[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  const int64_t local = e - P.voff[lo];
+  if (local < 0 || local >= P.numel[lo]) return;  // alignment gap between tensors
+  const TV v = load_tv<false>(op, P, lo);
+  typename Op::Frag f;
+  op.template load<false>(v, local, 0u, f);
+  op.template apply<false>(v, local, 0u, f, acc);
+}
+
+// The same with the span's descriptors staged in LDS (the north star's "LDS
+// staging for small-tensor gather"): the first `span` lanes each load one
+// tensor's extent [voff, voff + numel) and its descriptor (stream pointers,
+// alignment bits) into LDS, then every lane binary-searches LDS instead of
+// chasing log2(span) dependent global loads and reads its tensor's descriptor
+// from LDS instead of gathering it.  Runs of small tensors (BN weights /
+// biases, tensor tails) are the chunks this serves; spans above kMixedStage
+// (runs of tiny or empty tensors) keep the global path.  The caller's branch
+// is uniform across the workgroup (the chunk's code), so the barriers are too.
+// Measured: profiles/r2mlds/ (tiny tensors pack -15 %, R50 neutral).
+#ifndef GS_MIXED_LDS
+#define GS_MIXED_LDS 1
+#endif
+constexpr int kMixedStage = 64;  // tensors per mixed chunk staged (5 KB of LDS)
+template <class Op>
+__device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
+                                                float& acc, int64_t* s_lo, int64_t* s_hi, TV* s_tv) {
+  __syncthreads();  // the previous mixed chunk's lanes are done with the stage
+  if (static_cast<int>(threadIdx.x) < span) {
+    const int t = t0 + static_cast<int>(threadIdx.x);
+    const TV d = load_tv<false>(op, P, t);
+    s_lo[threadIdx.x] = P.voff[t];
+    s_hi[threadIdx.x] = P.voff[t] + d.numel;
+    s_tv[threadIdx.x] = d;
+  }
+  __syncthreads();
+  const int64_t e = c * kChunkElems + static_cast<int>(threadIdx.x) * kUnit;
+  int lo = 0, hi = span - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_lo[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  const int64_t local = e - s_lo[lo];
+  if (local < 0 || e >= s_hi[lo]) return;  // alignment gap between tensors
+  const TV v = s_tv[lo];
+  typename Op::Frag f;
+  op.template load<false>(v, local, 0u, f);
+  op.template apply<false>(v, local, 0u, f, acc);
+}
+
+template <int G, class Op>
+__device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int t, int64_t c0, float& acc) {
+  // G chunks c0 .. c0+G-1, all inside tensor t
+  const TV v = load_tv<true>(op, P, t);
+  const int64_t e0 = c0 * kChunkElems - cload(P.voff, t);
+  const uint32_t tid = threadIdx.x;
+  typename Op::Frag f[G];
+  if (op.fast_ok(v)) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template apply<true>(v, e0, j * kChunkElems + tid * kUnit, f[j], acc);
+  } else {
+    // a stream is not 16-B aligned: the checked path over the same range
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template load<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template apply<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j], acc);
+  }
+}
+
+template <class Op>
+__global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, Op op) {
+  static_assert(Op::kN == kUnit, "the chunk engine moves 4 elements per lane-access");
+  constexpr int G = Op::kG;
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "group of 1, 2, 4 or 8 chunks");
+  float acc = 0.f;
+  load_hyper(op);            // uniform: graph-replayable lr / bias corrections, clip coefficient
+  if (!op.active()) return;  // uniform across the grid
+  __shared__ int64_t s_lo[kMixedStage], s_hi[kMixedStage];  // mixed chunks: the span's extents
+  __shared__ TV s_tv[kMixedStage];                            // ... and descriptors
+  const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
+  const int* cw = &P.chunks[0].t0;  // [t0, code] pairs
+  // groups per workgroup: grid-stride (per_wg == 0) or a contiguous range
+  const int64_t g_begin = P.per_wg ? blockIdx.x * static_cast<int64_t>(P.per_wg) : blockIdx.x;
+  const int64_t g_end = P.per_wg ? std::min<int64_t>(n_groups, g_begin + P.per_wg) : n_groups;
+  const int64_t g_step = P.per_wg ? 1 : gridDim.x;
+  for (int64_t g = g_begin; g < g_end; g += g_step) {
+    const int64_t c0 = g * G;
+    const int t = cload(cw, 2 * c0);
+    const int code = cload(cw, 2 * c0 + 1);
+    if constexpr (G > 1) {
+      // the whole group inside one tensor: first and last chunk full in t
+      if (code == 0 && c0 + G <= P.n_chunks && cload(cw, 2 * (c0 + G - 1)) == t &&
+          cload(cw, 2 * (c0 + G - 1) + 1) == 0) {
+        chunk_full<G>(op, P, t, c0, acc);
+        continue;
+      }
+    }
+    for (int j = 0; j < G; ++j) {
+      const int64_t c = c0 + j;
+      if (c >= P.n_chunks) break;
+      const int tj = j == 0 ? t : cload(cw, 2 * c);
+      const int cj = j == 0 ? code : cload(cw, 2 * c + 1);
+      if (cj == 0) chunk_full<1>(op, P, tj, c, acc);
+      else if (GS_MIXED_LDS && cj > 0 && cj <= kMixedStage) chunk_mixed_lds(op, P, tj, cj, c, acc, s_lo, s_hi, s_tv);
+      else if (cj > 0) chunk_mixed(op, P, tj, cj, c, acc);
+    }
+  }
+  if constexpr (Op::kRed != 0) {
+    constexpr bool MAX = Op::kRed == 2;
+    const float r = block_reduce<MAX>(acc);
+    if (!P.red_fuse) {
+      if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+      return;
+    }
+    // In-kernel combine, two-level ticket.  Workgroup b belongs to group
+    // b mod R (R = P.red_fuse, a power of two <= kRedMaxGroups; with R a
+    // multiple of 8 a group's workgroups share the round-robin XCD of their
+    // dispatch: speed only, nothing assumes it).  Each group has its own
+    // arrival counter on its own 128-B line, so no device-scope word sees
+    // more than grid/R arrivals (one word serialises them at ~12 ns each —
+    // MI355X_MICROARCH.md "fanin"; the single-counter form measured 2.4 TB/s,
+    // r2c).  The partial goes out write-through (agent-scope store), the
+    // storing wave drains it (vmcnt(0)), then arrives; the group's last
+    // arriver folds the group's partials (agent-scope loads) in block order,
+    // publishes the group sum the same way and arrives on the top counter;
+    // the last group folds the R group sums in group order.  Every counter is
+    // re-armed by its last arriver.  The result depends only on the grid and
+    // R, not on arrival order: deterministic, so ranks reducing identical
+    // grads agree bit for bit.  Hand-off form: MI355X_MICROARCH.md's table,
+    // row 1 (sc1 stores, vmcnt(0), atomic add, sc1 loads), no fences.
+    constexpr int kStride = kRedSyncStride;
+    __shared__ int s_role;  // 0: done, 1: group leader, 2: also the last group
+    const int R = P.red_fuse;
+    const int k = static_cast<int>(blockIdx.x) & (R - 1);
+    const int grid = static_cast<int>(gridDim.x);
+    const int n_groups = grid < R ? grid : R;
+    uint32_t* top = &P.ticket[kRedMaxGroups * kStride];
+    float* gsums = reinterpret_cast<float*>(P.ticket + (kRedMaxGroups + 1) * kStride);
+    if (threadIdx.x == 0) {
+      const uint32_t ng = static_cast<uint32_t>((grid - 1 - k) / R + 1);
+      __hip_atomic_store(&op.partials[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(&P.ticket[k * kStride], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      s_role = tk == ng - 1;
+    }
+    __syncthreads();
+    if (!s_role) return;  // uniform within the workgroup
+    float v = 0.f;
+    for (int i = k + R * static_cast<int>(threadIdx.x); i < grid; i += R * kBlock) {
+      const float x = __hip_atomic_load(&op.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = MAX ? fmaxf(v, x) : v + x;
+    }
+    const float gsum = block_reduce<MAX>(v);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&P.ticket[k * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gsums[k * kStride], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (P.red_groups_only) {
+        // gs_sqnorm_partial: the group sums are the result; the clipped update
+        // on this plan folds them (clip_multiplier), no top-level hand-off.
+        // gs_sqnorm_partial_out: also contiguous in caller memory (a stream-
+        // ordered consumer: the ranks' all-reduce, then the update)
+        if (P.red_out) P.red_out[k] = gsum;
+        s_role = 0;
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_role = tk == static_cast<uint32_t>(n_groups) - 1 ? 2 : 0;
+      }
+    }
+    __syncthreads();
+    if (s_role != 2 || threadIdx.x >= 64) return;
+    // the last group: wave 0 folds the group sums (lane j: group j, j + 64, ...)
+    float t = 0.f;
+    for (int j = static_cast<int>(threadIdx.x); j < n_groups; j += 64) {
+      const float x = __hip_atomic_load(&gsums[j * kStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = MAX ? fmaxf(t, x) : t + x;
+    }
+    const float tot = MAX ? wave_max(t) : wave_sum(t);
+    if (threadIdx.x == 0) {
+      float* out = P.red_out;
+      if (MAX) out[0] = P.red_acc ? fmaxf(out[0], tot) : tot;
+      else out[0] = P.red_acc ? out[0] + tot : tot;
+      __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Which ops stream through the chunk-map engine (bit 1 << GS_OP_*); the rest
+// use the task engine.  GS_ENGINE=<mask> overrides (A/B runs).
+#ifndef GS_CHUNK_OPS
+#define GS_CHUNK_OPS 254
+#endif
+bool use_chunk_engine(int kind) {
+  static const int mask = [] {
+    const char* e = std::getenv("GS_ENGINE");
+    return e ? std::atoi(e) : GS_CHUNK_OPS;
+  }();
+  return (mask >> kind) & 1;
+}
+// reductions: at most Op::kRedGrid workgroups (= partials for the combine:
+// 8 Ki for the read-only Σg² / inf checks, uncapped for the unpack that
+// carries a fused Σg²; profiles/r2e_red.jsonl), each grid-striding or taking a
+// contiguous range of groups (GS_RED_CONTIG=1); GS_RED_GRID / GS_RED_CONTIG
+// in the environment override (sweeps)
+#ifndef GS_RED_CONTIG
+#define GS_RED_CONTIG 0
+#endif
+int red_grid_cap(int op_default) {
+  static const int v = [] {
+    const char* e = std::getenv("GS_RED_GRID");
+    return e ? std::max(1, std::min(std::atoi(e), kGridLimit)) : 0;
+  }();
+  return v > 0 ? v : op_default;
+}
+// in-kernel combine groups (0 = the combine_partials launch); GS_RED_FUSE=<R>
+int red_fuse_groups() {
+  static const int v = [] {
+    const char* e = std::getenv("GS_RED_FUSE");
+    int r = e ? std::atoi(e) : GS_RED_FUSE;
+    if (r <= 0) return 0;
+    int p2 = 1;
+    while (p2 < r && p2 < kRedMaxGroups) p2 <<= 1;
+    return p2;
+  }();
+  return v;
+}
+bool red_contiguous() {
+  static const bool v = [] {
+    const char* e = std::getenv("GS_RED_CONTIG");
+    return e ? std::atoi(e) != 0 : GS_RED_CONTIG != 0;
+  }();
+  return v;
+}
+
+// ---------------------------------------------------------------- ops
+template <int DT>
+__device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
+  return static_cast<char*>(flat) + off * (DT == GS_F32 ? 4 : 2);
+}
+
+// Op access convention: load<F> / apply<F>(tv, e0, lo, frag[, acc]) handle the
+// 4 (or kN) elements starting at element e0 + lo of tensor tv.  F = true is
+// the chunk engine's full-chunk path (e0 wave-uniform, no bounds checks, every
+// stream 16-B aligned: `fast_ok` says when a tensor qualifies); F = false is
+// the general path with bounds / alignment checks (lo = 0 there).
+
+// MODE (GS_SCALE_NONE / _MUL / _DIV) is a template parameter: a runtime mode
+// left a uniform branch and the unused IEEE-division path inside every
+// lane-step of the streaming loop
+template <int N, int SD, int FD, int MODE>
+struct PackOp {
+  static constexpr int kN = N;
+  static constexpr int kG = FD == GS_F32 ? GS_G_PACK : GS_G_PACK16;
+  static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kKind = GS_OP_PACK;
+  float* partials = nullptr;
+  int slot;
+  void* flat;
+  bool flat_vec;
+  float s;
+  struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const {
+    return flat_vec && (v.off % 4) == 0 && (v.ptr[0] == nullptr || v.vec(0));
+  }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    const void* src = v.ptr[0];
+    if (src == nullptr) {  // unused parameter (find_unused_parameters): pack zeros
+      for (int i = 0; i < N; ++i) f.x[i] = 0.f;
+      return;
+    }
+    ld<SD, N, F>(src, e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float x = f.x[i];
+      if constexpr (MODE == GS_SCALE_MUL) {
+        x = x * s;
+      } else if constexpr (MODE == GS_SCALE_DIV) {
+        // bf16_compress_hook order: round to the bucket dtype, then divide
+        x = round_to<FD>(x) / s;
+      }
+      f.x[i] = x;
+    }
+    st<FD, N, F>(flat_at<FD>(flat, v.off), e0, lo, v.numel, flat_vec && (v.off % N) == 0, f.x);
+  }
+};
+
+// RED = 1: Σ dst² of the written values (fused grad-norm); RED = 2: non-finite
+// flag of the written values (fused AMP inf check, max-combined into the flag)
+template <int N, int FD, int DD, int RED = 1>
+struct UnpackOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_UNPACK;
+  static constexpr int kRed = RED;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kKind = GS_OP_UNPACK;
+  float* partials = nullptr;
+  bool want_red;
+  const void* flat;
+  bool flat_vec;
+  int slot;
+  struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const {
+    return flat_vec && (v.off % 4) == 0 && (v.ptr[0] == nullptr || v.vec(0));
+  }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<FD, N, F>(flat_at<FD>(const_cast<void*>(flat), v.off), e0, lo, v.numel,
+                 flat_vec && (v.off % N) == 0, f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float& acc) const {
+    void* dst = v.ptr[0];
+    if (dst == nullptr) return;  // unused parameter: grad left untouched
+    st<DD, N, F>(dst, e0, lo, v.numel, v.vec(0), f.x);
+    if (want_red) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float r = round_to<DD>(f.x[i]);
+        if constexpr (RED == 1) acc = fmaf(r, r, acc);
+        else if ((F || e0 + lo + i < v.numel) && !isfinite(r)) acc = 1.f;
+      }
+    }
+  }
+};
+
+template <int N, int DT>
+struct ScaleOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_UNPACK;
+  static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kKind = GS_OP_SCALE;
+  float* partials = nullptr;
+  int slot;
+  float s;
+  int mode;
+  struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) f.x[i] = (mode == GS_SCALE_DIV) ? f.x[i] / s : f.x[i] * s;
+    st<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+};
+
+template <int N, int DT>
+struct SqnormOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
+  static constexpr int kRed = 1;
+  static constexpr int kRedGrid = 8192;
+  static constexpr int kKind = GS_OP_SQNORM;
+  float* partials = nullptr;
+  int slot;
+  struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV&, int64_t, uint32_t, Frag& f, float& acc) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc = fmaf(f.x[i], f.x[i], acc);
+  }
+};
+
+// Σ x (debug bucket checksums)
+template <int N, int DT>
+struct SumOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
+  static constexpr int kRed = 1;
+  static constexpr int kRedGrid = 8192;
+  static constexpr int kKind = GS_OP_SUM;
+  float* partials = nullptr;
+  int slot;
+  struct Frag { float x[N]; };
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV&, int64_t, uint32_t, Frag& f, float& acc) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc += f.x[i];
+  }
+};
+
+template <int N, int DT>
+struct UnscaleOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_RED;
+  static constexpr int kRed = 2;
+  static constexpr int kRedGrid = 8192;
+  static constexpr int kKind = GS_OP_UNSCALE;
+  float* partials = nullptr;
+  int slot;
+  const float* inv;  // nullable
+  struct Frag { float x[N]; };
+  // logical slot 0 = the op's table row `slot` (descriptor loads, gs_kernels.hip: load_tv)
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return true; }
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float& acc) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if ((F || e0 + lo + i < v.numel) && !isfinite(f.x[i])) acc = 1.f;
+    if (inv) {
+      const float s = *inv;
+      if (s != 1.f) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) f.x[i] = f.x[i] * s;
+        st<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+      }
+    }
+  }
+};
+
+// SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
+// NTG / NTS: non-temporal loads of the grad / of p and the momentum buffer (above)
+template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
+struct SgdOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_SGD;
+  static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kKind = GS_OP_SGD;
+  float* partials = nullptr;
+  SgdHyper h;
+  const float* gscale;
+  const float* found_inf;
+  const float* hyper = nullptr;  // [lr] in device memory (gs_plan_set_hyper_source)
+  ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
+  bool clip_on = false;
+  bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
+  float gsv = 1.f;
+  struct Frag { float p[N], g[N], b[N]; };
+  __device__ int phys(int k) const { return k; }
+  __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
+  __device__ bool fast_ok(const TV& v) const {
+    return v.vec(0) && v.vec(1) && (h.mom == 0.f || v.vec(2)) && (LD < 0 || v.vec(3));
+  }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
+    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float g = f.g[i];
+      if (use_gs) g = g * gsv;                      // clip_grad_norm_ / unscale: grads *= coef
+      if (h.maximize) g = -g;
+      if (h.wd != 0.f) g = fmaf(h.wd, f.p[i], g);   // grad.add(param, alpha=wd)
+      float d = g;
+      if (h.mom != 0.f) {
+        // buf = clone(g) on the first step, else buf.mul_(mom).add_(g, alpha=1-damp)
+        const float b = h.first ? g : fmaf(h.omd, g, f.b[i] * h.mom);
+        f.b[i] = b;
+        d = h.nesterov ? fmaf(h.mom, b, g) : b;     // g.add(buf, alpha=mom)
+      }
+      f.p[i] = fmaf(-h.lr, d, f.p[i]);              // param.add_(d, alpha=-lr)
+    }
+    st<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    if (h.mom != 0.f) st<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+    if constexpr (LD >= 0) st<LD, N, F>(v.ptr[3], e0, lo, v.numel, v.vec(3), f.p);
+  }
+};
+
+// Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
+template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
+struct AdamOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_ADAM;
+  static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kKind = GS_OP_ADAM;
+  float* partials = nullptr;
+  AdamHyper h;
+  const float* gscale;
+  const float* found_inf;
+  const float* hyper = nullptr;  // [step_size, bc2_sqrt, 1 - lr*wd] in device memory
+  ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
+  bool clip_on = false;
+  bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
+  float gsv = 1.f;
+  struct Frag { float p[N], g[N], m[N], v[N]; };
+  __device__ int phys(int k) const { return k; }
+  __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
+  __device__ bool fast_ok(const TV& tv) const {
+    return tv.vec(0) && tv.vec(1) && tv.vec(2) && tv.vec(3) && (LD < 0 || tv.vec(4));
+  }
+  template <bool F>
+  __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
+    ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+  }
+  template <bool F>
+  __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float g = f.g[i];
+      if (use_gs) g = g * gsv;
+      if (h.maximize) g = -g;
+      float p = f.p[i];
+      if (h.wd != 0.f) {
+        if (h.adamw) p = p * h.decay;                       // param.mul_(1 - lr*wd)
+        else g = fmaf(h.wd, p, g);                          // grad.add(param, alpha=wd)
+      }
+      const float m = fmaf(h.w1, g - f.m[i], f.m[i]);       // exp_avg.lerp_(g, 1-b1)  (w<0.5)
+      const float v = fmaf(h.w2 * g, g, f.v[i] * h.b2);     // mul_(b2).addcmul_(g, g, 1-b2)
+      const float denom = sqrtf(v) / h.bc2s + h.eps;        // sqrt(v)/bc2_sqrt + eps
+      p = fmaf(h.step_size, m / denom, p);                  // addcdiv_(m, denom, -lr/bc1)
+      f.p[i] = p; f.m[i] = m; f.v[i] = v;
+    }
+    st<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    st<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    st<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+    if constexpr (LD >= 0) st<LD, N, F>(tv.ptr[4], e0, lo, tv.numel, tv.vec(4), f.p);
+  }
+};
+
+// The update's grad multiplier, formed once per workgroup (uniform): *gscale
+// (AMP unscale / a precomputed clip coefficient) or, with a folded clip, the
+// clip coefficient itself — from a finished Σg² or from the Σg² kernel's group
+// sums (lane j reads group j and the wave folds them: the fused combine's own
+// last step, so the result is bit-identical to gs_sqnorm's), then exactly
+// clip_coef_kernel's arithmetic.  Workgroup 0 publishes [Σg², coef, norm].
+__device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float* gscale) {
+  float sq;
+  if (c.groups > 0) {
+    const int l = static_cast<int>(threadIdx.x & 63);
+    const float x = l < c.groups ? c.sq[l * c.stride] : 0.f;
+    sq = wave_sum(0.f + x);
+  } else {
+    sq = c.sq[0];
+  }
+  const float s = gscale ? *gscale : 1.f;
+  if (gscale) sq = sq * (s * s);                    // the norm of the unscaled grads
+  sq = sq * c.sq_mul;
+  const float nrm = sqrtf(sq);
+  float coef = c.max_norm / (nrm + c.eps);
+  coef = coef < 1.f ? coef : 1.f;
+  if (gscale) coef = coef * s;
+  coef = coef * c.coef_mul;
+  if (c.out && blockIdx.x == 0 && threadIdx.x == 0) {
+    c.out[0] = sq;
+    c.out[1] = coef;
+    c.out[2] = nrm;
+  }
+  return coef;
+}
+template <class Op>
+__device__ __forceinline__ void load_grad_multiplier(Op& op) {
+  op.use_gs = op.gscale != nullptr || op.clip_on;
+  op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
+}
+template <int N, int GD, int LD, bool NTG, bool NTS>
+__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTG, NTS>& op) {
+  if (op.hyper) {
+    op.h.lr = op.hyper[0];
+    if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
+  }
+  load_grad_multiplier(op);
+}
+template <int N, int GD, int LD, bool NTG, bool NTS>
+__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTG, NTS>& op) {
+  if (op.hyper) {
+    op.h.step_size = op.hyper[0];
+    op.h.bc2s = op.hyper[1];
+    op.h.decay = op.hyper[2];
+  }
+  load_grad_multiplier(op);
+}
+
+__global__ void clip_coef_kernel(const float* sq, float max_norm, float eps, float* coef,
+                                 float* norm) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float nrm = sqrtf(sq[0]);
+    if (norm) norm[0] = nrm;
+    const float c = max_norm / (nrm + eps);
+    coef[0] = c < 1.f ? c : 1.f;
+  }
+}
+
+// ------------------------------------------------------------- launching
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      (void)hipSetDevice(dev);
+    } else {
+      prev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// groups_only (gs_sqnorm_partial): the fused reduction stops at its R group
+// sums, which stay in the plan for the next clipped update (p->red_groups)
+template <int ILP, class Op>
+int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0,
+           int groups_only = 0) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->n == 0 || p->segs.empty()) {
+    if (Op::kRed != 0 && red_out && !accumulate) HIP_RET(hipMemsetAsync(red_out, 0, 4, s));
+    return GS_OK;
+  }
+  {
+    GsRange r("gs_plan_flush");
+    GS_TRY_RET(hip_plan_flush(p, stream));
+  }
+  GsRange r_launch("gs_kernel_launch");
+  op.partials = p->d_partials;
+  const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
+  const int tk = p->timer_next;
+  if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
+  const bool chunk = use_chunk_engine(Op::kKind) && !p->chunks.empty();
+  int grid = p->grid;
+  bool fused = false;
+  if (chunk) {
+    const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
+    const bool red = Op::kRed != 0 && (red_out || groups_only);
+    int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
+    // groups_only is asked for only when the ordinary reduction would fuse too
+    // (hip_sqnorm_partial), so both fold the same R group sums of the same grid
+    fused = red && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
+    if (fused) cap = std::min(cap, red_grid_cap(GS_RED_FUSE_GRID));
+    // any fused reduction overwrites the group sums a gs_sqnorm_partial left
+    if (fused && !groups_only) p->red_valid = false;
+    grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
+    PlanArgs a = p->args();
+    a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
+    a.red_out = Op::kRed != 0 ? red_out : nullptr;  // groups_only: the contiguous group sums (nullable)
+    a.red_acc = accumulate;
+    a.red_fuse = fused ? red_fuse_groups() : 0;
+    a.red_groups_only = groups_only;
+    if (groups_only) p->red_groups = std::min(grid, red_fuse_groups());
+    a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
+    hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
+  } else {
+    hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
+  }
+  HIP_RET(hipGetLastError());
+  if constexpr (Op::kRed != 0) {
+    if (red_out && !fused) {
+      hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s,
+                         (const float*)p->d_partials, grid, red_out, accumulate);
+      HIP_RET(hipGetLastError());
+    }
+  }
+  if (nslots) {
+    HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]), s));
+    p->timer_kind[tk] = Op::kKind;
+    p->timer_next = (tk + 1) % nslots;
+    p->timer_count = std::min(p->timer_count + 1, nslots);
+  }
+  HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), s));
+  p->last_stream = stream;
+  p->last_captured = stream_capturing(s);
+  return GS_OK;
+}
+
+bool flat_aligned(const void* flat) { return (reinterpret_cast<uintptr_t>(flat) & 15u) == 0; }
+
+}  // namespace
+
+#define GS_DISPATCH_FLOAT(DT, NAME, ...)                        \
+  switch (DT) {                                                 \
+    case GS_F32: { constexpr int NAME = GS_F32; __VA_ARGS__; break; }   \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; } \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }   \
+    default: return fail(GS_EINVAL, "unsupported floating dtype");      \
+  }
+
+#define GS_DISPATCH_LOWP(DT, NAME, ...)                                  \
+  switch (DT) {                                                          \
+    case -1: { constexpr int NAME = -1; __VA_ARGS__; break; }            \
+    case GS_BF16: { constexpr int NAME = GS_BF16; __VA_ARGS__; break; }  \
+    case GS_F16: { constexpr int NAME = GS_F16; __VA_ARGS__; break; }    \
+    default: return fail(GS_EINVAL, "unsupported low-precision dtype");  \
+  }
+
+}  // namespace gs
