@@ -20,6 +20,7 @@
 
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1270,6 +1271,19 @@ struct DeviceGuard {
   }
 };
 
+// The plan launch timer (gs_plan_timer_enable) takes the kernel's own start and
+// end: hipExtLaunchKernel's events, written by the dispatch itself, instead of two
+// event packets queued around it, whose own processing added ~3 µs to every timed
+// launch (a fifth of a 17 µs Σg² kernel, profiles/r4/r4i_timer_ext.jsonl).
+// GS_TIMER_EXT=0 brings the packet pair back (A/B).
+bool timer_ext() {
+  static const bool v = [] {
+    const char* e = std::getenv("GS_TIMER_EXT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // groups_only (gs_sqnorm_partial): the fused reduction stops at its R group
 // sums, which stay in the plan for the next clipped update (p->red_groups)
 template <int ILP, class Op>
@@ -1288,7 +1302,10 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   op.partials = p->d_partials;
   const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
-  if (nslots) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk]), s));
+  const bool ext = nslots && timer_ext();
+  hipEvent_t ev0 = nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk]) : nullptr;
+  hipEvent_t ev1 = nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]) : nullptr;
+  if (nslots && !ext) HIP_RET(hipEventRecord(ev0, s));
   const bool chunk = use_chunk_engine(Op::kKind) && !p->chunks.empty();
   int grid = p->grid;
   bool fused = false;
@@ -1311,20 +1328,34 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     a.red_groups_only = groups_only;
     if (groups_only) p->red_groups = std::min(grid, red_fuse_groups());
     a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
-    hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
+    const bool combine = Op::kRed != 0 && red_out && !fused;
+    if (ext)
+      hipExtLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, ev0, combine ? nullptr : ev1, 0, a,
+                            op);
+    else
+      hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
   } else {
-    hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
+    const bool combine = Op::kRed != 0 && red_out;
+    if (ext)
+      hipExtLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, ev0, combine ? nullptr : ev1, 0,
+                            p->args(), op);
+    else
+      hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
   }
   HIP_RET(hipGetLastError());
   if constexpr (Op::kRed != 0) {
     if (red_out && !fused) {
-      hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s,
-                         (const float*)p->d_partials, grid, red_out, accumulate);
+      if (ext)
+        hipExtLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s, nullptr, ev1, 0,
+                              (const float*)p->d_partials, grid, red_out, accumulate);
+      else
+        hipLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s,
+                           (const float*)p->d_partials, grid, red_out, accumulate);
       HIP_RET(hipGetLastError());
     }
   }
   if (nslots) {
-    HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]), s));
+    if (!ext) HIP_RET(hipEventRecord(ev1, s));
     p->timer_kind[tk] = Op::kKind;
     p->timer_next = (tk + 1) % nslots;
     p->timer_count = std::min(p->timer_count + 1, nslots);
