@@ -112,7 +112,7 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 // Non-temporal loads in the fused updates (profiles/r4/r4c_nt_instep.jsonl,
 // r4e_nt_state.jsonl: bench.py in the training step + the beyond-Infinity-Cache
 // rows, library variants interleaved, two rounds):
-// * the read-once gradient stream: unless a folded clip's Σg² pass read it just before
+// * the read-once gradient stream: unless a Σg² pass of the plan read it just before
 //   (in-step ResNet-50 SGD 0.786 -> 0.805-0.816 of 8 TB/s; back-to-back ResNet-152 x 2
 //   SGD 0.709 -> 0.729; but the clip path's update, right behind the Σg² kernel that
 //   brought the grads into the caches, 0.770 -> 0.740 with NT grad loads);

@@ -351,6 +351,7 @@ int gs_sqnorm(gs_plan* p, int slot, int dtype, float* sqnorm_dev, int accumulate
   PLAN_OK(p);
   SLOT_OK(slot);
   GS_CHECK_ARG(sqnorm_dev != nullptr, "gs_sqnorm: NULL output");
+  p->grads_read = slot == 1;
   if (p->kind == GS_DEV_HOST) return host_sqnorm(p, slot, dtype, sqnorm_dev, accumulate);
   return hip_sqnorm(p, slot, dtype, sqnorm_dev, accumulate, stream);
 }
@@ -360,6 +361,7 @@ int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream) {
   PLAN_OK(p);
   SLOT_OK(slot);
   p->red_valid = true;
+  p->grads_read = slot == 1;
   if (p->kind == GS_DEV_HOST) {
     p->red_groups = 0;
     return host_sqnorm(p, slot, dtype, &p->h_red, 0);
@@ -374,6 +376,7 @@ int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, in
   SLOT_OK(slot);
   GS_CHECK_ARG(groups_out != nullptr && n_groups != nullptr, "gs_sqnorm_partial_out: NULL argument");
   p->red_valid = true;
+  p->grads_read = slot == 1;
   if (p->kind == GS_DEV_HOST) {
     p->red_groups = 0;
     GS_TRY_RET(host_sqnorm(p, slot, dtype, &p->h_red, 0));

@@ -18,8 +18,13 @@ static bool nt_state(const gs_plan* p, int state_streams) {
   return n * 4 * (1 + state_streams) > kInfinityCacheBytes;
 }
 
-// grads read just before by a folded clip's Σg² kernel stay in the caches: cached loads
-static bool nt_grad(const ClipArgs* clip) { return GS_NT_LOAD_GRAD != 0 && clip == nullptr; }
+// grads a Σg² pass of this plan read just before (the clip path) stay in the caches:
+// cached loads then, non-temporal otherwise (the flag is consumed by the update)
+static bool nt_grad(gs_plan* p) {
+  const bool hot = p->grads_read;
+  p->grads_read = false;
+  return GS_NT_LOAD_GRAD != 0 && !hot;
+}
 
 template <bool NTG, bool NTS>
 static int sgd_nt(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
@@ -36,7 +41,7 @@ static int sgd_nt(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* 
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
             const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  const bool ntg = nt_grad(clip), nts = nt_state(p, h.mom != 0.f ? 1 : 0);
+  const bool ntg = nt_grad(p), nts = nt_state(p, h.mom != 0.f ? 1 : 0);
   if (ntg) return nts ? sgd_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
                       : sgd_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
   return nts ? sgd_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
@@ -58,7 +63,7 @@ static int adam_nt(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
              const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  const bool ntg = nt_grad(clip), nts = nt_state(p, 2);
+  const bool ntg = nt_grad(p), nts = nt_state(p, 2);
   if (ntg) return nts ? adam_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
                       : adam_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
   return nts ? adam_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)

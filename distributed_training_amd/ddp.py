@@ -393,6 +393,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._comm_hook: tuple[Any, Callable] | None = None
         self._buffers_plan = None
         self._sqnorm_target: torch.Tensor | None = None
+        self._sqnorm_valid = False  # the last synchronising backward's unpacks filled _sqnorm_target
         self._found_inf_target: torch.Tensor | None = None
         self._found_inf_valid = False
 
@@ -517,6 +518,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         if self._post_bwd_futs:
             self._wait_post_backward_futures()
         self._found_inf_valid = self._found_inf_target is not None
+        self._sqnorm_valid = self._sqnorm_fusable()
         if self.gradient_as_bucket_view:
             b = self._bucketer
             for i, p in enumerate(self._params):
@@ -782,6 +784,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         else:
             self.require_forward_param_sync = False
             self._found_inf_valid = False  # grads will change without a synchronising unpack
+            self._sqnorm_valid = False
         return output
 
     def _prepare_for_backward(self):
@@ -798,6 +801,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         if self._found_inf_target is not None:
             self._found_inf_target.zero_()  # on the producer stream, before any bucket is launched
         self._found_inf_valid = False
+        self._sqnorm_valid = False
         L.check(L.lib().gs_bucketer_prepare(self._bucketer.handle, None if sq is None else sq.data_ptr()),
                 "gs_bucketer_prepare")
         self._in_backward = True
@@ -940,6 +944,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             # bucketer has unpacked them at finalize — step every bucket then
             self._overlap_step(range(len(b.buckets)))
         self._found_inf_valid = self._found_inf_target is not None
+        self._sqnorm_valid = self._sqnorm_fusable()
         if self.find_unused_parameters:
             if self.world_size > 1:
                 self._grads_of_locally_unused()
@@ -1159,8 +1164,17 @@ class DistributedDataParallel(nn.Module, Joinable):
                 "gs_bucketer_set_found_inf")
 
     def set_grad_sqnorm_target(self, t: torch.Tensor | None):
-        """Fuse Σg² of the averaged grads into the unpack (fp32 1-element tensor)."""
+        """Fuse Σg² of the averaged grads into the bucket unpack (fp32 1-element
+        device tensor; the first bucket's unpack writes it, the others add, in
+        bucket order); ``_sqnorm_valid`` tells whether the last synchronising
+        backward filled it (not in ``gradient_as_bucket_view`` mode: no unpack)."""
+        if t is not None and (t.numel() != 1 or t.dtype != torch.float32 or t.device != self.device):
+            raise ValueError("Σg² target must be a 1-element float32 tensor on the DDP device")
         self._sqnorm_target = t
+        self._sqnorm_valid = False
+
+    def _sqnorm_fusable(self) -> bool:
+        return self._sqnorm_target is not None and not self.gradient_as_bucket_view
 
     def set_timeline(self, level: int):
         """Which HIP timing events the bucket chains record

@@ -95,6 +95,7 @@ class _FusedBase(torch.optim.Optimizer):
         self.grad_scale: torch.Tensor | None = None
         self.found_inf: torch.Tensor | None = None
         self._clip_buf: dict = {}
+        self._norm_ddp = None  # fuse_grad_norm_into: (ddp, its parameter ids)
         self._dev_hyper: dict = {}  # param-group index -> device hyper-parameter buffers
         self._dense_seen: dict = {}  # id(param) -> strides already checked dense
 
@@ -156,6 +157,38 @@ class _FusedBase(torch.optim.Optimizer):
         a group already keeps its counters there."""
         return self.capturable or self.found_inf is not None or bool(self._dev_hyper)
 
+    def fuse_grad_norm_into(self, ddp):
+        """Let ``ddp`` (libgsync DistributedDataParallel over exactly this
+        optimizer's parameters) compute Σg² of the averaged grads inside its
+        bucket unpacks ("partial ‖g‖² fused into unpack"); the
+        clipped step then folds that scalar and runs no Σg² pass of its own —
+        the clip path's exposed end is the update alone.  The sum runs in bucket
+        order instead of the plan's, so the coefficient equals the unfused one
+        to fp32 rounding.  Steps without a fresh synchronising backward (no_sync
+        accumulation, ``gradient_as_bucket_view``, another parameter set) take
+        the unfused path."""
+        if not self.defaults.get("max_grad_norm"):
+            raise ValueError("fuse_grad_norm_into: the optimizer has no max_grad_norm")
+        dev = ddp.device
+        buf = self._clip_buf.get(dev)
+        if buf is None:
+            buf = self._clip_buf[dev] = torch.zeros(4, dtype=torch.float32, device=dev)
+        ddp.set_grad_sqnorm_target(buf[3:4])
+        self._norm_ddp = (ddp, frozenset(id(p) for p in ddp._params))
+
+    def _ddp_sqnorm(self, device):
+        """The DDP's fused Σg² when it covers this step's grads (consumed)."""
+        if self._norm_ddp is None:
+            return None
+        ddp, ids = self._norm_ddp
+        if not ddp._sqnorm_valid or ddp.device != device:
+            return None
+        mine = frozenset(id(p) for g in self.param_groups for p in g["params"] if p.grad is not None)
+        if mine != ids:
+            return None
+        ddp._sqnorm_valid = False
+        return self._clip_buf[device][3:4]
+
     def _clip_scale(self, device, all_plans):
         """DeepSpeed-style gradient_clipping folded into the update: returns the
         grad multiplier the update launches get.
@@ -182,6 +215,15 @@ class _FusedBase(torch.optim.Optimizer):
         sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
         self.last_grad_norm = norm
         if CLIP_FUSED:
+            fused = self._ddp_sqnorm(device)
+            if fused is not None:
+                # Σg² already formed by the DDP's unpacks: no pass over the grads here
+                for plan, _ in all_plans:
+                    plan.set_clip(float(max_norm), 1e-6, fused, out=buf[0:3])
+                    plan._clip_on = True
+                self.last_clip_source = "ddp_unpack"
+                return self.grad_scale
+            self.last_clip_source = "optimizer"
             if len(all_plans) == 1:
                 plan, gdt = all_plans[0]
                 plan.sqnorm_partial(1, gdt)

@@ -331,3 +331,106 @@ def test_folded_clip_equals_separate_path_reduction_overrides_gpu(env):
     r = subprocess.run([sys.executable, "-c", _RED_FUSE_CHILD.format(repo=repo)], env={**os.environ, **env},
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def _ddp_fused_norm(rank, ws, device="cpu", steps=4):
+    """FusedSGD.fuse_grad_norm_into(ddp): Σg² of the averaged grads formed inside
+    the DDP's bucket unpacks (several buckets, accumulated in bucket order), the
+    clipped update folding that scalar — against the same DDP + clipped FusedSGD
+    whose Σg² pass runs in the optimizer: published norms within fp32 rounding
+    (rtol 1e-6: the two sums add the same squares in another order), weights within
+    SURVEY §8c's SGD bound (rtol 1e-5, atol 1e-7), with a no_sync accumulation step
+    (synchronised by the next backward) and the ranks' weights identical."""
+    import torch.distributed as dist
+
+    from tests.test_ddp_cpu import _micro
+
+    dev = torch.device(device)
+    torch.manual_seed(0)
+    m1, m2 = _micro().to(dev), _micro().to(dev)
+    m2.load_state_dict(m1.state_dict())
+    a = D.DistributedDataParallel(m1, bucket_cap_mb=0.05)
+    b = D.DistributedDataParallel(m2, bucket_cap_mb=0.05)
+    oa = D.FusedSGD(a.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, max_grad_norm=0.5)
+    ob = D.FusedSGD(b.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, max_grad_norm=0.5)
+    oa.fuse_grad_norm_into(a)
+    g = torch.Generator().manual_seed(7 + rank)
+    for it in range(steps):
+        xs = [torch.rand(4, 3, 32, 32, generator=g).to(dev) for _ in range(2)]
+        ys = [torch.randint(0, 10, (4,), generator=g).to(dev) for _ in range(2)]
+        if it == 2:
+            for model in (a, b):
+                with model.no_sync():
+                    torch.nn.functional.cross_entropy(model(xs[0]), ys[0]).backward()
+        for model in (a, b):
+            torch.nn.functional.cross_entropy(model(xs[1]), ys[1]).backward()
+        oa.step()
+        ob.step()
+        assert oa.last_clip_source == "ddp_unpack" and ob.last_clip_source == "optimizer", it
+        na, nb = oa.last_grad_norm.item(), ob.last_grad_norm.item()
+        assert abs(na - nb) <= 1e-6 * nb, (it, na, nb)
+        for (n, pa), pb in zip(m1.named_parameters(), m2.parameters()):
+            torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-7, msg=f"it {it} {n}")
+        oa.zero_grad()
+        ob.zero_grad()
+    # a step without a fresh synchronising backward falls back to the optimizer's own pass
+    torch.nn.functional.cross_entropy(a(xs[1]), ys[1]).backward()
+    oa.step()
+    oa.step()
+    assert oa.last_clip_source == "optimizer"
+    w = torch.cat([p.detach().reshape(-1).cpu() for p in m1.parameters()])
+    allw = [torch.zeros_like(w) for _ in range(ws)]
+    dist.all_gather(allw, w)
+    assert all(torch.equal(allw[0], x) for x in allw[1:])
+
+
+def test_ddp_fused_grad_norm_cpu_ws2():
+    from tests.test_ddp_cpu import _run
+
+    _run(_ddp_fused_norm, 2)
+
+
+def _gpu_fused_norm_worker(rank, ws, backend, port, errq):
+    try:
+        from tests._dist_util import init_pg
+
+        init_pg(backend, rank, ws, port)
+        torch.cuda.set_device(0)
+        _ddp_fused_norm(rank, ws, "cuda")
+        import torch.distributed as dist
+
+        dist.barrier()
+        if backend == "nccl":
+            from distributed_training_amd.comm import destroy_communicators
+
+            destroy_communicators()
+        dist.destroy_process_group()
+    except BaseException as e:
+        import traceback
+
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend,ws", [("nccl", 1), ("gloo", 2)])
+def test_ddp_fused_grad_norm_gpu(backend, ws):
+    """The same on the GPU: RCCL at ws=1 (the bucketer's own collective and
+    unpacks) and two ranks sharing the GPU over gloo (host-staged buckets)."""
+    import torch.multiprocessing as mp
+
+    from tests._dist_util import free_port
+
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = free_port()
+    procs = [ctx.Process(target=_gpu_fused_norm_worker, args=(r, ws, backend, port, errq)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
