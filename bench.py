@@ -235,7 +235,16 @@ def _kernel_rows(shapes, dev, iters):
             ("sqnorm_f32", 4 * n, lambda: plan.sqnorm(1, torch.float32, sq))):
         ms = rate(fn, plan)
         rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9}
-    del flat, flat16
+    # the 16-bit bucket paths: ZeRO's bf16 grads -> bf16 bucket (configs[3]) and the bf16
+    # bucket -> fp32 grads unpack (DDP bucket_dtype=bf16)
+    grads16 = [gr.to(torch.bfloat16) for gr in grads]
+    plan.set_ptrs(1, grads16)
+    ms = rate(lambda: plan.pack(1, torch.bfloat16, flat16, 0.125, 1), plan)
+    rows["pack_bf16"] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9}
+    plan.set_ptrs(1, grads)
+    ms = rate(lambda: plan.unpack(flat16, 1, torch.float32), plan)
+    rows["unpack_bf16_to_f32"] = {"alg_bytes": 6 * n, "avg_ms": ms, "GBps": 6 * n / (ms * 1e-3) / 1e9}
+    del flat, flat16, grads16
     up = TensorListPlan(numels, dev, task_units=update_task_units(dev))
     ps = [torch.randn(s, device=dev, generator=g) for s in shapes]
     bs = [torch.randn(s, device=dev, generator=g) * 0.01 for s in shapes]

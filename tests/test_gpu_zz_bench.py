@@ -66,7 +66,8 @@ def _check_line(d, n):
     # every grad-sync kernel alone on the model's params (the north star's >= 70 % covers them all)
     k = d["grad_sync_kernels"]
     assert set(k["kernels"]) == {"pack_f32", "pack_f32_to_bf16", "unpack_f32", "unpack_f32+sqnorm", "sqnorm_f32",
-                                 "sgd_momentum_wd", "sqnorm_partial_f32", "clip_path_sgd", "adam"}
+                                 "pack_bf16", "unpack_bf16_to_f32", "sgd_momentum_wd", "sqnorm_partial_f32",
+                                 "clip_path_sgd", "adam"}
     # the folded clip path: Σg² partials + the clipped update, both launches in one row
     assert k["kernels"]["clip_path_sgd"]["alg_bytes"] == 24 * d["config"]["params"]
     assert k["kernels"]["clip_path_sgd"]["avg_ms"] > k["kernels"]["sgd_momentum_wd"]["avg_ms"]
