@@ -413,9 +413,9 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
     n_big, big = _kernel_rows(_beyond_ic_shapes(), dev, iters)
     torch.cuda.empty_cache()
     out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS,
-           "timing": "after the timed region, warm, alone on the GPU; plan launch timer (HIP events on the "
-                     f"launch stream around each kernel), average of {iters} calls (kernel-trace durations: "
-                     "profiles/r3/r3i_trace_rates.json)",
+           "timing": "after the timed region, warm, alone on the GPU; plan launch timer (the kernels' own start "
+                     "and end: hipExtLaunchKernel's HIP events on the launch stream; GS_TIMER_EXT=0 = an event "
+                     f"pair around the launch), average of {iters} calls",
            "min_frac": min(r["frac"] for r in rows.values()),
            "beyond_ic": {"params": n_big, "set": "ResNet-152 parameter shapes x 2 (> 256 MiB Infinity Cache)",
                          "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}
@@ -1132,7 +1132,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
                 "avg_launch_ms": opt_ms_avg,
                 "launches": len(opt_ms),
-                "timing": ("libgsync plan launch timer: HIP events recorded on the launch stream around each kernel"
+                "timing": ("libgsync plan launch timer: the kernel's own start / end, hipExtLaunchKernel's HIP events "
+                           "on the launch stream (GS_TIMER_EXT=0: an event pair around the launch)"
                            + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
                            + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
                               if args.optimizer_overlap else "")),

@@ -6,8 +6,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r4i; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py \
-  tests/test_clip_fold.py tests/test_zero_ds_step.py tests/test_gpu_large.py > $OUT/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread tests/test_clip_fold.py tests/test_gpu_kernels.py \
+  tests/test_zero_ds_step.py tests/test_gpu_large.py > $OUT/pytest.log 2>&1
 rc=$?; tail -3 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do
   for ext in 1 0; do

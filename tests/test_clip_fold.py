@@ -378,10 +378,11 @@ def _ddp_fused_norm(rank, ws, device="cpu", steps=4):
     oa.step()
     oa.step()
     assert oa.last_clip_source == "optimizer"
-    w = torch.cat([p.detach().reshape(-1).cpu() for p in m1.parameters()])
-    allw = [torch.zeros_like(w) for _ in range(ws)]
-    dist.all_gather(allw, w)
-    assert all(torch.equal(allw[0], x) for x in allw[1:])
+    if ws > 1:
+        w = torch.cat([p.detach().reshape(-1).cpu() for p in m1.parameters()])
+        allw = [None] * ws
+        dist.all_gather_object(allw, w)
+        assert all(torch.equal(allw[0], x) for x in allw[1:])
 
 
 def test_ddp_fused_grad_norm_cpu_ws2():
@@ -396,6 +397,9 @@ def _gpu_fused_norm_worker(rank, ws, backend, port, errq):
 
         init_pg(backend, rank, ws, port)
         torch.cuda.set_device(0)
+        # both models must see the same grads: MIOpen's default backward is not
+        # run-to-run deterministic (that alone moved the norms by 3e-6)
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
         _ddp_fused_norm(rank, ws, "cuda")
         import torch.distributed as dist
 
