@@ -1021,7 +1021,8 @@ def main():
                                "frac_at_trace_duration": bytes_per_param * upd_params / (tr["avg_us"] * 1e-6)
                                / 1e9 / HBM_PEAK_GBPS,
                                "source": "profiles/trace_roofline.json: rocprofv3 kernel trace of the timed "
-                                         "launches of this command (the event pair adds the kernel's dispatch)"}
+                                         "launches of this command on a committed run (the profiler's per-kernel "
+                                         "completion handling adds a few µs; box-to-box spread ±4 %)"}
         except Exception:
             trace_check = None
     if torch_zero:

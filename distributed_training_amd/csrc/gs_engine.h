@@ -167,7 +167,10 @@ constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too 
 #define GS_G_PACK 1     // fp32 bucket
 #endif
 #ifndef GS_G_PACK16
-#define GS_G_PACK16 8   // 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
+#define GS_G_PACK16 8   // fp32 grads -> 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
+#endif
+#ifndef GS_G_PACK16_16
+#define GS_G_PACK16_16 8  // 16-bit grads -> 16-bit bucket (ZeRO's bf16 pack)
 #endif
 #ifndef GS_G_UNPACK
 #define GS_G_UNPACK 2
@@ -888,7 +891,7 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
 template <int N, int SD, int FD, int MODE>
 struct PackOp {
   static constexpr int kN = N;
-  static constexpr int kG = FD == GS_F32 ? GS_G_PACK : GS_G_PACK16;
+  static constexpr int kG = FD == GS_F32 ? GS_G_PACK : (SD == GS_F32 ? GS_G_PACK16 : GS_G_PACK16_16);
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
   static constexpr int kKind = GS_OP_PACK;
