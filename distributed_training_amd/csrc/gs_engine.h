@@ -170,7 +170,7 @@ constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too 
 #define GS_G_PACK16 8   // fp32 grads -> 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
 #endif
 #ifndef GS_G_PACK16_16
-#define GS_G_PACK16_16 8  // 16-bit grads -> 16-bit bucket (ZeRO's bf16 pack)
+#define GS_G_PACK16_16 4  // 16-bit grads -> 16-bit bucket, ZeRO's bf16 pack (r4k sweep: 4 > 2 > 8 > 1)
 #endif
 #ifndef GS_G_UNPACK
 #define GS_G_UNPACK 2
