@@ -894,6 +894,7 @@ struct PackOp {
   static constexpr int kG = FD == GS_F32 ? GS_G_PACK : (SD == GS_F32 ? GS_G_PACK16 : GS_G_PACK16_16);
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_PACK;
   float* partials = nullptr;
   int slot;
@@ -941,6 +942,7 @@ struct UnpackOp {
   static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = RED;
   static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = 8192;  // its fused Σg² / inf check: <= 2 groups per workgroup (r4l)
   static constexpr int kKind = GS_OP_UNPACK;
   float* partials = nullptr;
   bool want_red;
@@ -981,6 +983,7 @@ struct ScaleOp {
   static constexpr int kG = GS_G_UNPACK;
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_SCALE;
   float* partials = nullptr;
   int slot;
@@ -1009,6 +1012,7 @@ struct SqnormOp {
   static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 1;
   static constexpr int kRedGrid = 8192;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_SQNORM;
   float* partials = nullptr;
   int slot;
@@ -1035,6 +1039,7 @@ struct SumOp {
   static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 1;
   static constexpr int kRedGrid = 8192;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_SUM;
   float* partials = nullptr;
   int slot;
@@ -1059,6 +1064,7 @@ struct UnscaleOp {
   static constexpr int kG = GS_G_RED;
   static constexpr int kRed = 2;
   static constexpr int kRedGrid = 8192;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_UNSCALE;
   float* partials = nullptr;
   int slot;
@@ -1096,6 +1102,7 @@ struct SgdOp {
   static constexpr int kG = GS_G_SGD;
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_SGD;
   float* partials = nullptr;
   SgdHyper h;
@@ -1148,6 +1155,7 @@ struct AdamOp {
   static constexpr int kG = GS_G_ADAM;
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
   static constexpr int kKind = GS_OP_ADAM;
   float* partials = nullptr;
   AdamHyper h;
@@ -1315,11 +1323,18 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   if (chunk) {
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
     const bool red = Op::kRed != 0 && (red_out || groups_only);
-    int cap = red ? std::min(p->grid_cap, red_grid_cap(Op::kRedGrid)) : p->grid_cap;
+    // a streaming op carrying a reduction (the unpack's Σg² / inf check) runs one group
+    // per workgroup; up to 16 Ki groups (a ResNet-50 gradient, any DDP bucket) it
+    // combines in-kernel on an 8 Ki grid rather than through a second launch
+    // (profiles/r4/r4l_red_grid.jsonl: ResNet-50 0.70 -> 0.78; ResNet-152 x 2 stays
+    // uncapped + combine launch, 0.76 vs 0.71)
+    const int op_cap = (Op::kRedGrid == kGridLimit && groups <= 2 * kRedFuseMaxGrid) ? kRedFuseMaxGrid
+                                                                                       : Op::kRedGrid;
+    int cap = red ? std::min(p->grid_cap, red_grid_cap(op_cap)) : p->grid_cap;
     // groups_only is asked for only when the ordinary reduction would fuse too
     // (hip_sqnorm_partial), so both fold the same R group sums of the same grid
     fused = red && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
-    if (fused) cap = std::min(cap, red_grid_cap(GS_RED_FUSE_GRID));
+    if (fused) cap = std::min(cap, red_grid_cap(Op::kRedFuseGrid));
     // any fused reduction overwrites the group sums a gs_sqnorm_partial left
     if (fused && !groups_only) p->red_valid = false;
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
