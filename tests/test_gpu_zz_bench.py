@@ -12,6 +12,7 @@ module is named to run after the other GPU modules."""
 import json
 import os
 import socket
+import signal
 import subprocess
 import sys
 
@@ -38,6 +39,39 @@ def _env():
     env["MASTER_ADDR"] = "127.0.0.1"
     env["MASTER_PORT"] = str(_port())
     return env
+
+
+class _Result:
+    def __init__(self, returncode, stdout, stderr):
+        self.returncode, self.stdout, self.stderr = returncode, stdout, stderr
+
+
+def _run(cmd, env, timeout):
+    """Run a bench child; its stderr (the "[bench] ..." progress lines and the
+    ranks' logs) goes to a file — under $GSYNC_TEST_PROGRESS_DIR when set
+    (scripts/gpu_tests.sh points it into gpurun_out/, so a long multi-rank run
+    shows progress instead of looking silent), else a temp file — and is read
+    back for the assertion messages."""
+    import tempfile
+
+    d = os.environ.get("GSYNC_TEST_PROGRESS_DIR") or tempfile.gettempdir()
+    os.makedirs(d, exist_ok=True)
+    name = os.environ.get("PYTEST_CURRENT_TEST", "bench").split(" ")[0].replace("/", "_").replace("::", "__")
+    path = os.path.join(d, f"{name}.{os.getpid()}.err")
+    with open(path, "w") as err:
+        # own session: on a timeout the whole group (torchrun and its ranks) is killed, not only the launcher
+        p = subprocess.Popen(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=err, text=True,
+                             start_new_session=True)
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            out, _ = p.communicate()
+            with open(path) as f:
+                raise AssertionError(f"bench child exceeded {timeout} s; stderr tail:\n{f.read()[-6000:]}")
+    with open(path) as f:
+        stderr = f.read()
+    return _Result(p.returncode, out, stderr)
 
 
 def _json_lines(out):
@@ -91,8 +125,7 @@ def _check_line(d, n):
 
 
 def test_bench_n1_contract(cuda_device):
-    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL, cwd=REPO, env=_env(),
-                       capture_output=True, text=True, timeout=400)
+    p = _run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL, _env(), 400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]
@@ -110,7 +143,7 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            "bench.py", "--gpus", "2", "--pg-backend", "gloo"] + SMALL
-    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=500)
+    p = _run(cmd, env, 500)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
@@ -149,8 +182,8 @@ def _check_policy_ab(d, n):
 def test_bench_policy_ab_n1_rccl(cuda_device):
     """The same A/B forced on at N=1 over libgsync's RCCL communicator (the
     comm-side code of the driver's run: re-wrapping, close(), the standalone leg)."""
-    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1", "--policy-ab", "1", "--kernel-rates", "0"]
-                       + SMALL, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=400)
+    p = _run([sys.executable, "-u", "bench.py", "--gpus", "1", "--policy-ab", "1", "--kernel-rates", "0"] + SMALL,
+             _env(), 400)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json_lines(p.stdout)[0]
     _check_policy_ab(d, 1)
@@ -160,8 +193,8 @@ def test_bench_policy_ab_n1_rccl(cuda_device):
 def test_bench_colossal_engine(cuda_device):
     """BASELINE configs[4]'s path: the Colossal Booster shim as run.sh drives it
     (TorchDDPPlugin, fp16 mixed precision, HybridAdam) through bench.py."""
-    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1", "--engine", "colossal", "--kernel-rates", "0"]
-                       + SMALL, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=400)
+    p = _run([sys.executable, "-u", "bench.py", "--gpus", "1", "--engine", "colossal", "--kernel-rates", "0"] + SMALL,
+             _env(), 400)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json_lines(p.stdout)[0]
     assert d["config"]["engine"] == "colossal" and d["dtype"] == "fp16"
@@ -181,8 +214,7 @@ def test_bench_collective_bench_leg(cuda_device, engine):
     DDP with the overlapped optimizer, the parity step after it."""
     extra = ["--collective-bench", "1", "--kernel-rates", "0"]
     extra += ["--optimizer-overlap", "1"] if engine == "ddp" else ["--engine", "zero2"]
-    p = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL + extra, cwd=REPO, env=_env(),
-                       capture_output=True, text=True, timeout=400)
+    p = _run([sys.executable, "-u", "bench.py", "--gpus", "1"] + SMALL + extra, _env(), 400)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json_lines(p.stdout)[0]
     sb = d["grad_sync"]["standalone"]
@@ -209,7 +241,9 @@ def test_bench_multirank_gloo_rehearsal(cuda_device, engine, n):
            "bench.py", "--gpus", str(n), "--pg-backend", "gloo", "--kernel-rates", "0"] + SMALL
     if engine == "zero2":
         cmd += ["--engine", "zero2"]
-    p = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=600)
+    # a healthy run takes ~30 s; a hung one dumps every rank's stacks each 40 s into the stderr file
+    # (under gpurun_out/ in scripts/gpu_tests.sh, so the box sees output) and fails before pytest's 300 s
+    p = _run(cmd, dict(_env(), GSYNC_BENCH_TRACEBACK_S="40"), 270)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
@@ -232,7 +266,7 @@ def test_bench_wall_budget_skips_legs_keeps_the_headline(cuda_device):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--wall-budget-s", "1", "--kernel-rates", "0",
            "--policy-ab", "1"] + SMALL
-    p = subprocess.run(cmd, cwd=REPO, env=_env(), capture_output=True, text=True, timeout=500)
+    p = _run(cmd, _env(), 500)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]
@@ -251,7 +285,7 @@ def test_bench_leg_watchdog_exits_nonzero_keeps_the_headline(cuda_device):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            "bench.py", "--gpus", "2", "--pg-backend", "gloo", "--wall-budget-s", "1", "--kernel-rates", "0"] + SMALL
     env = dict(_env(), GSYNC_BENCH_TEST_HANG_LEG="parity")
-    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=500)
+    p = _run(cmd, env, 500)
     assert p.returncode != 0, "a leg overrunning the budget must not look like a clean run"
     lines = _json_lines(p.stdout)
     assert len(lines) == 1, p.stdout[-2000:]
