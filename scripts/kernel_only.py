@@ -3,7 +3,8 @@ launches — the unit a rocprofv3 PMC pass (FETCH_SIZE / WRITE_SIZE) measures.
     python scripts/kernel_only.py <model> <launches> <op> [replicas]
 op: sgd | adam (update plan, as FusedSGD / FusedAdam build it), clipsgd (the folded clip
     path on the update plan: gs_sqnorm_partial + the clipped SGD, max_norm 1.0),
-    pack | pack16 | unpack | unpacksq | sqnorm | sqpart (bucket-layout plan, align 64;
+    pack | pack16 | pack16b | unpack | unpacksq | sqnorm | sqpart (bucket-layout plan, align 64;
+    pack16 = fp32 grads -> bf16 bucket, pack16b = bf16 grads -> bf16 bucket (ZeRO-2's pack);
     sqpart = gs_sqnorm_partial, the folded clip's Σg² launch)."""
 import os
 import sys
@@ -21,7 +22,8 @@ reps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 dev = torch.device("cuda", 0)
 shapes = [p.shape for p in MODELS[model]().parameters()] * reps
 n = [torch.Size(s).numel() for s in shapes]
-gs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
+gdt = torch.bfloat16 if op == "pack16b" else torch.float32
+gs = [(torch.randn(s, device=dev) * 0.01).to(gdt) for s in shapes]
 if op in ("sgd", "adam", "clipsgd"):
     ps = [torch.randn(s, device=dev) for s in shapes]
     bs = [torch.randn(s, device=dev) * 0.01 for s in shapes]
@@ -32,7 +34,7 @@ if op in ("sgd", "adam", "clipsgd"):
 else:
     plan = TensorListPlan(n, dev, align=64)
     plan.set_ptrs(1, gs)
-    flat = torch.zeros(plan.flat_numel, device=dev, dtype=torch.bfloat16 if op == "pack16" else torch.float32)
+    flat = torch.zeros(plan.flat_numel, device=dev, dtype=torch.bfloat16 if op in ("pack16", "pack16b") else torch.float32)
     sq = torch.zeros(1, device=dev)
 for _ in range(iters):
     if op == "adam":
@@ -43,8 +45,8 @@ for _ in range(iters):
         plan.sqnorm_partial(1, torch.float32)
         plan.set_clip(1.0)
         plan.sgd(torch.float32, 1e-6, 0.9, 0.0, 1e-4, False, False, False)
-    elif op in ("pack", "pack16"):
-        plan.pack(1, torch.float32, flat, 0.125, 1)
+    elif op in ("pack", "pack16", "pack16b"):
+        plan.pack(1, gdt, flat, 0.125, 1)
     elif op == "unpack":
         plan.unpack(flat, 1, torch.float32)
     elif op == "unpacksq":

@@ -10,7 +10,7 @@ import os
 import sys
 
 
-KERNEL = {"sgd": "SgdOp", "adam": "AdamOp", "pack": "PackOp", "pack16": "PackOp", "unpack": "UnpackOp",
+KERNEL = {"sgd": "SgdOp", "adam": "AdamOp", "pack": "PackOp", "pack16": "PackOp", "pack16b": "PackOp", "unpack": "UnpackOp",
           "unpacksq": "UnpackOp", "sqnorm": "SqnormOp", "sqpart": "SqnormOp",
           "clipsgd": "SgdOp"}  # clipsgd: the clipped update's own dispatches (its Σg² launch is sqpart)
 
