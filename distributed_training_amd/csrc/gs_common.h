@@ -182,6 +182,7 @@ struct gs_plan {
   int n = 0;
   int64_t align_elems = 0;
   int64_t flat_numel = 0;
+  int64_t elems = 0;                   // Σ numel (the load policy's stream sizes)
   std::vector<int64_t> numel, off;
   std::vector<gs::Seg> segs;
   std::vector<int32_t> task_begin;

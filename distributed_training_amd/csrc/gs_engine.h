@@ -129,6 +129,25 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #define GS_NT_STATE_DEFAULT 0
 #endif
 constexpr int64_t kInfinityCacheBytes = 256ll << 20;
+
+// A stream read once (the gradient in Σg²) takes non-temporal loads when it is
+// larger than the Infinity Cache: none of it can still be resident from its
+// producer, and the NT path streams faster (a plain read-only float4 sum beyond
+// the cache: 0.84-0.87 of 8 TB/s NT vs 0.72-0.76 cached, scripts/micro/stream_mix.hip,
+// profiles/r4/r4p_stream_mix_*.jsonl).  At or below the cache size the loads stay
+// cached: the grads were just written and are largely resident (NT cost the
+// ResNet-50 rows 2-10 %, r4b).  GS_NT_READ_ONCE=0 never, 1 always, 2 the size rule.
+#ifndef GS_NT_READ_ONCE_DEFAULT
+#define GS_NT_READ_ONCE_DEFAULT 2
+#endif
+inline bool nt_read_once(int64_t stream_bytes) {
+  static const int policy = [] {
+    const char* e = std::getenv("GS_NT_READ_ONCE");
+    return e ? std::atoi(e) : GS_NT_READ_ONCE_DEFAULT;
+  }();
+  return policy == 2 ? stream_bytes > kInfinityCacheBytes : policy != 0;
+}
+inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
 #ifndef GS_NT_STORE
 #define GS_NT_STORE 1
 #endif
@@ -1006,7 +1025,9 @@ struct ScaleOp {
   }
 };
 
-template <int N, int DT>
+// NT: non-temporal loads (a read-once stream larger than the Infinity Cache,
+// nt_read_once below)
+template <int N, int DT, bool NT = false>
 struct SqnormOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_RED;
@@ -1023,7 +1044,7 @@ struct SqnormOp {
   __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+    ld<DT, N, F, NT>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
   template <bool F>
   __device__ void apply(const TV&, int64_t, uint32_t, Frag& f, float& acc) const {

@@ -266,14 +266,24 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
   return GS_OK;
 }
 
-int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
-  DeviceGuard g(p->device);
+template <bool NT>
+static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
-    SqnormOp<GS_PACK_N, DT> op;
+    SqnormOp<GS_PACK_N, DT, NT> op;
     op.slot = slot;
-    return launch<GS_RED_ILP>(p, op, stream, sq, acc);
+    return launch<GS_RED_ILP>(p, op, stream, sq, acc, groups_only);
   });
   return GS_OK;
+}
+// the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once)
+static int sqnorm_launch(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
+  return nt_read_once(p->elems * dtype_bytes(dt)) ? sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream)
+                                                  : sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
+}
+
+int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
+  DeviceGuard g(p->device);
+  return sqnorm_launch(p, slot, dt, sq, acc, 0, stream);
 }
 
 // Σ x² of one slot left in the plan for a clipped update (gs_sqnorm_partial):
@@ -296,22 +306,17 @@ int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t*
   const int cap = std::min(p->grid_cap, red_grid_cap(SqnormOp<GS_PACK_N, GS_F32>::kRedGrid));
   const bool groups = use_chunk_engine(GS_OP_SQNORM) && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
                       red_fuse_groups() > 0 && cap <= kRedFuseMaxGrid;
-  GS_DISPATCH_FLOAT(dt, DT, {
-    SqnormOp<GS_PACK_N, DT> op;
-    op.slot = slot;
-    if (groups) {
-      GS_TRY_RET(launch<GS_RED_ILP>(p, op, stream, groups_out, 0, 1));
-      if (n_groups) *n_groups = p->red_groups;
-      return GS_OK;
-    }
-    p->red_groups = 0;
-    if (n_groups) *n_groups = 1;
-    GS_TRY_RET(launch<GS_RED_ILP>(p, op, stream, hip_plan_red_scalar(p), 0));
-    if (groups_out)
-      HIP_RET(hipMemcpyAsync(groups_out, hip_plan_red_scalar(p), sizeof(float), hipMemcpyDeviceToDevice,
-                             static_cast<hipStream_t>(stream)));
+  if (groups) {
+    GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 1, stream));
+    if (n_groups) *n_groups = p->red_groups;
     return GS_OK;
-  });
+  }
+  p->red_groups = 0;
+  if (n_groups) *n_groups = 1;
+  GS_TRY_RET(sqnorm_launch(p, slot, dt, hip_plan_red_scalar(p), 0, 0, stream));
+  if (groups_out)
+    HIP_RET(hipMemcpyAsync(groups_out, hip_plan_red_scalar(p), sizeof(float), hipMemcpyDeviceToDevice,
+                           static_cast<hipStream_t>(stream)));
   return GS_OK;
 }
 

@@ -169,6 +169,7 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
     cur = rup(cur);
     p->off[t] = cur;
     cur += numels[t];
+    p->elems += numels[t];
   }
   p->flat_numel = rup(cur);
   // segments and tasks

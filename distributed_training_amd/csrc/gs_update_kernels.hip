@@ -13,15 +13,14 @@ static bool nt_state(const gs_plan* p, int state_streams) {
     return e ? std::atoi(e) : GS_NT_STATE_DEFAULT;
   }();
   if (policy != 2) return policy != 0;
-  int64_t n = 0;
-  for (int64_t x : p->numel) n += x;
-  return n * 4 * (1 + state_streams) > kInfinityCacheBytes;
+  return p->elems * 4 * (1 + state_streams) > kInfinityCacheBytes;
 }
 
-// grads a Σg² pass of this plan read just before (the clip path) stay in the caches:
-// cached loads then, non-temporal otherwise (the flag is consumed by the update)
-static bool nt_grad(gs_plan* p) {
-  const bool hot = p->grads_read;
+// grads a Σg² pass of this plan read just before (the clip path) stay in the caches
+// when they fit in the Infinity Cache: cached loads then, non-temporal otherwise
+// (the flag is consumed by the update)
+static bool nt_grad(gs_plan* p, int gdt) {
+  const bool hot = p->grads_read && p->elems * dtype_bytes(gdt) <= kInfinityCacheBytes;
   p->grads_read = false;
   return GS_NT_LOAD_GRAD != 0 && !hot;
 }
@@ -41,7 +40,7 @@ static int sgd_nt(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* 
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gsc, const float* fi,
             const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  const bool ntg = nt_grad(p), nts = nt_state(p, h.mom != 0.f ? 1 : 0);
+  const bool ntg = nt_grad(p, gdt), nts = nt_state(p, h.mom != 0.f ? 1 : 0);
   if (ntg) return nts ? sgd_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
                       : sgd_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
   return nts ? sgd_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
@@ -63,7 +62,7 @@ static int adam_nt(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float
 int hip_adam(gs_plan* p, int gdt, int ldt, const AdamHyper& h, const float* gsc, const float* fi,
              const ClipArgs* clip, void* stream) {
   DeviceGuard g(p->device);
-  const bool ntg = nt_grad(p), nts = nt_state(p, 2);
+  const bool ntg = nt_grad(p, gdt), nts = nt_state(p, 2);
   if (ntg) return nts ? adam_nt<true, true>(p, gdt, ldt, h, gsc, fi, clip, stream)
                       : adam_nt<true, false>(p, gdt, ldt, h, gsc, fi, clip, stream);
   return nts ? adam_nt<false, true>(p, gdt, ldt, h, gsc, fi, clip, stream)

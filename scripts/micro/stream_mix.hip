@@ -1,0 +1,143 @@
+// Ceiling probe for the update kernels beyond the Infinity Cache: how fast does
+// a plain grid of float4 lanes stream the same read / write mix as the fused
+// SGD (p, g, momentum read; p, momentum written in place = 3R2W, 20 B/elem) and
+// the fp32 Adam (4R3W, 28 B/elem), next to copy (1R1W) and a read-only sum (1R),
+// with no chunk map, no descriptors, no tensor boundaries?  Loads cached or
+// non-temporal, stores non-temporal or plain, G accesses in flight per lane,
+// one-shot grid (one G-group per workgroup, as libgsync's chunk engine) or a
+// resident grid-stride grid.  ResNet-152 x 2 elements (120.4 M, 2.4 GB per SGD
+// launch: > 9x the 256 MiB cache), back-to-back launches timed by an event pair
+// each (the beyond_ic harness's conditions).  One JSON line per case.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ f4 ld(const f4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(f4* p, f4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// R streams read (s[0..R-1]); the first W of them written back in place
+template <int R, int W, int G, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256) mix(f4* __restrict__ s0, f4* __restrict__ s1, f4* __restrict__ s2,
+                                          f4* __restrict__ s3, int64_t n4, float* __restrict__ part) {
+  f4* s[4] = {s0, s1, s2, s3};
+  const int64_t step = (int64_t)gridDim.x * 256 * G;
+  float acc = 0.f;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * G; base < n4; base += step) {
+    f4 v[G][R];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + (int64_t)g * 256 + threadIdx.x;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[g][r] = i < n4 ? ld<NTL>(s[r] + i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + (int64_t)g * 256 + threadIdx.x;
+      if constexpr (W == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc += v[g][r].x + v[g][r].y + v[g][r].z + v[g][r].w;
+      } else if (i < n4) {
+        if constexpr (R == 1) {
+          st<NTS>(s[1] + i, v[g][0]);  // copy: s0 -> s1
+        } else if constexpr (R == 3) {
+          const f4 m = v[g][2] * 0.9f + v[g][1];  // SGD: buf = mu buf + g; p -= lr buf
+          st<NTS>(s[2] + i, m);
+          st<NTS>(s[0] + i, v[g][0] - 1e-6f * m);
+        } else {
+          const f4 m = v[g][2] * 0.9f + v[g][1] * 0.1f;  // Adam-shaped: m, v, p
+          const f4 q = v[g][3] * 0.999f + v[g][1] * v[g][1] * 0.001f;
+          st<NTS>(s[2] + i, m);
+          st<NTS>(s[3] + i, q);
+          st<NTS>(s[0] + i, v[g][0] - 1e-6f * m / (q + 1e-8f));
+        }
+      }
+    }
+  }
+  if constexpr (W == 0) {
+    if (acc == 12345.f) part[blockIdx.x] = acc;  // keeps the loads; never true for zeros
+  }
+}
+
+template <class K>
+static float time_ms(K launch, int iters) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int i = 0; i < 3; ++i) launch();
+  float tot = 0.f;
+  for (int i = 0; i < iters; ++i) {
+    hipEventRecord(a, 0);
+    launch();
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    tot += ms;
+  }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return tot / iters;
+}
+
+int main() {
+  const int64_t n = 120385616 / 1024 * 1024;  // ResNet-152 x 2, whole 1 Ki chunks
+  const int64_t n4 = n / 4;
+  f4* s[4];
+  for (auto& p : s) {
+    if (hipMalloc(&p, n * 4)) {
+      printf("alloc failed\n");
+      return 1;
+    }
+    hipMemset(p, 0, n * 4);
+  }
+  float* part;
+  if (hipMalloc(&part, 65536 * 4)) return 1;
+  struct Case {
+    const char* name;
+    double bytes_per_elem;
+    float ms;
+    int grid;
+  };
+  std::vector<Case> cs;
+  for (int round = 0; round < 2; ++round) {
+    for (int gridc : {0, 2048, 8192}) {
+      auto g_of = [&](int G) { return gridc ? gridc : (int)std::min<int64_t>(1 << 30, (n4 + 256 * G - 1) / (256 * G)); };
+#define CASE(NAME, BPE, R, W, G, NTL, NTS)                                                                      \
+  cs.push_back({NAME, BPE,                                                                                      \
+                time_ms([&] { mix<R, W, G, NTL, NTS><<<g_of(G), 256>>>(s[0], s[1], s[2], s[3], n4, part); }, 20), \
+                gridc})
+      CASE("read_sum_g4", 4, 1, 0, 4, false, true);
+      CASE("read_sum_g4_ntl", 4, 1, 0, 4, true, true);
+      CASE("copy_g4", 8, 1, 1, 4, false, true);
+      CASE("copy_g4_ntl", 8, 1, 1, 4, true, true);
+      CASE("sgd3r2w_g2", 20, 3, 2, 2, false, true);
+      CASE("sgd3r2w_g4", 20, 3, 2, 4, false, true);
+      CASE("sgd3r2w_g4_ntl", 20, 3, 2, 4, true, true);
+      CASE("sgd3r2w_g4_plainst", 20, 3, 2, 4, false, false);
+      CASE("sgd3r2w_g4_ntl_plainst", 20, 3, 2, 4, true, false);
+      CASE("sgd3r2w_g8", 20, 3, 2, 8, false, true);
+      CASE("adam4r3w_g4", 28, 4, 3, 4, false, true);
+      CASE("adam4r3w_g4_ntl", 28, 4, 3, 4, true, true);
+#undef CASE
+    }
+  }
+  for (auto& c : cs) {
+    const double gbps = c.bytes_per_elem * n / (c.ms * 1e-3) / 1e9;
+    printf("{\"case\": \"%s\", \"elems\": %lld, \"grid\": %d, \"avg_ms\": %.5f, \"GBps\": %.1f, \"frac\": %.4f}\n", c.name,
+           (long long)n, c.grid, c.ms, gbps, gbps / 8000.0);
+  }
+  for (auto& p : s) hipFree(p);
+  hipFree(part);
+  return 0;
+}

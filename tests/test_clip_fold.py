@@ -333,6 +333,57 @@ def test_folded_clip_equals_separate_path_reduction_overrides_gpu(env):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
+_NT_READ_CHILD = r"""
+import hashlib, sys, torch
+sys.path.insert(0, {repo!r})
+import distributed_training_amd as D
+dev = torch.device("cuda", 0)
+sizes = [48 * 1024 * 1024, 1000, 24 * 1024 * 1024 + 7, 2048]  # 288 MiB of fp32 grads: above the cache
+gen = torch.Generator(device=dev).manual_seed(5)
+gs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
+ps = [torch.randn(k, device=dev, generator=gen) for k in sizes]
+bs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
+plan = D.multi_tensor.TensorListPlan(sizes, dev)
+for k, ts in enumerate((ps, gs, bs)):
+    plan.set_ptrs(k, ts)
+sq = torch.zeros(1, device=dev)
+plan.sqnorm(1, torch.float32, sq)
+out = torch.zeros(3, device=dev)
+plan.sqnorm_partial(1, torch.float32)
+plan.set_clip(0.5, 1e-6, None, 1.0, 1.0, out=out)
+plan.sgd(torch.float32, 0.1, 0.9, 0.0, 1e-4, False, False, False)
+torch.cuda.synchronize()
+h = hashlib.sha256()
+for t in ps + bs:
+    h.update(t.cpu().numpy().tobytes())
+print("RES", sq.item().hex(), out.cpu().numpy().tobytes().hex(), h.hexdigest())
+"""
+
+
+@pytest.mark.gpu
+def test_nt_read_once_policy_changes_no_bits_gpu():
+    """Σg², the folded clip's partials and the clipped SGD over a 288 MiB gradient
+    slot (above the Infinity Cache: the size rule's non-temporal loads) give the
+    same bits under GS_NT_READ_ONCE = 0 (cached), 1 (always NT) and the default
+    rule: the load policy moves the bytes differently, never the sum's order
+    (a child process per setting: the policy is read once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for pol in ("0", "1", None):
+        env = {k: v for k, v in os.environ.items() if k != "GS_NT_READ_ONCE"}
+        if pol is not None:
+            env["GS_NT_READ_ONCE"] = pol
+        r = subprocess.run([sys.executable, "-c", _NT_READ_CHILD.format(repo=repo)], env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        res.append([ln for ln in r.stdout.splitlines() if ln.startswith("RES")][0])
+    assert res[0] == res[1] == res[2], res
+
+
 def _ddp_fused_norm(rank, ws, device="cpu", steps=4):
     """FusedSGD.fuse_grad_norm_into(ddp): Σg² of the averaged grads formed inside
     the DDP's bucket unpacks (several buckets, accumulated in bucket order), the
