@@ -136,16 +136,22 @@ constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 // the cache: 0.84-0.87 of 8 TB/s NT vs 0.72-0.76 cached, scripts/micro/stream_mix.hip,
 // profiles/r4/r4p_stream_mix_*.jsonl).  At or below the cache size the loads stay
 // cached: the grads were just written and are largely resident (NT cost the
-// ResNet-50 rows 2-10 %, r4b).  GS_NT_READ_ONCE=0 never, 1 always, 2 the size rule.
+// ResNet-50 rows 2-10 %, r4b).  GS_NT_READ_ONCE=0 never, 1 always, 2 the size rule;
+// GS_NT_SQNORM overrides it for the Σg² kernels alone (A/B).
 #ifndef GS_NT_READ_ONCE_DEFAULT
 #define GS_NT_READ_ONCE_DEFAULT 2
 #endif
-inline bool nt_read_once(int64_t stream_bytes) {
+inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
   static const int policy = [] {
     const char* e = std::getenv("GS_NT_READ_ONCE");
     return e ? std::atoi(e) : GS_NT_READ_ONCE_DEFAULT;
   }();
-  return policy == 2 ? stream_bytes > kInfinityCacheBytes : policy != 0;
+  static const int policy_sq = [] {
+    const char* e = std::getenv("GS_NT_SQNORM");
+    return e ? std::atoi(e) : policy;
+  }();
+  const int pol = sqnorm ? policy_sq : policy;
+  return pol == 2 ? stream_bytes > kInfinityCacheBytes : pol != 0;
 }
 inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
 #ifndef GS_NT_STORE
@@ -907,7 +913,8 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
 // MODE (GS_SCALE_NONE / _MUL / _DIV) is a template parameter: a runtime mode
 // left a uniform branch and the unused IEEE-division path inside every
 // lane-step of the streaming loop
-template <int N, int SD, int FD, int MODE>
+// NT: non-temporal loads of the source (a read-once stream above the cache size, nt_read_once)
+template <int N, int SD, int FD, int MODE, bool NT = false>
 struct PackOp {
   static constexpr int kN = N;
   static constexpr int kG = FD == GS_F32 ? GS_G_PACK : (SD == GS_F32 ? GS_G_PACK16 : GS_G_PACK16_16);
@@ -934,7 +941,7 @@ struct PackOp {
       for (int i = 0; i < N; ++i) f.x[i] = 0.f;
       return;
     }
-    ld<SD, N, F>(src, e0, lo, v.numel, v.vec(0), f.x);
+    ld<SD, N, F, NT>(src, e0, lo, v.numel, v.vec(0), f.x);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -955,7 +962,8 @@ struct PackOp {
 
 // RED = 1: Σ dst² of the written values (fused grad-norm); RED = 2: non-finite
 // flag of the written values (fused AMP inf check, max-combined into the flag)
-template <int N, int FD, int DD, int RED = 1>
+// NT: non-temporal loads of the flat buffer (above the cache size, nt_read_once)
+template <int N, int FD, int DD, int RED = 1, bool NT = false>
 struct UnpackOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_UNPACK;
@@ -977,8 +985,8 @@ struct UnpackOp {
   }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<FD, N, F>(flat_at<FD>(const_cast<void*>(flat), v.off), e0, lo, v.numel,
-                 flat_vec && (v.off % N) == 0, f.x);
+    ld<FD, N, F, NT>(flat_at<FD>(const_cast<void*>(flat), v.off), e0, lo, v.numel,
+                     flat_vec && (v.off % N) == 0, f.x);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float& acc) const {

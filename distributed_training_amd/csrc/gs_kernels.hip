@@ -212,48 +212,64 @@ int hip_plan_flush(gs_plan* p, void* stream) {
 }
 
 // ------------------------------------------------------------- dispatchers
-template <int SD, int FD, int MODE>
+template <int SD, int FD, int MODE, bool NT>
 static int pack_mode(gs_plan* p, int src_slot, void* flat, float s, void* stream) {
-  PackOp<GS_PACK_N, SD, FD, MODE> op;
+  PackOp<GS_PACK_N, SD, FD, MODE, NT> op;
   op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s;
   return launch<GS_PACK_ILP>(p, op, stream);
 }
 
-int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
-             void* stream) {
-  DeviceGuard g(p->device);
+template <bool NT>
+static int pack_nt(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
+                   void* stream) {
   GS_DISPATCH_FLOAT(src_dt, SD, GS_DISPATCH_FLOAT(flat_dt, FD, {
     switch (mode) {
-      case GS_SCALE_NONE: return pack_mode<SD, FD, GS_SCALE_NONE>(p, src_slot, flat, s, stream);
-      case GS_SCALE_MUL: return pack_mode<SD, FD, GS_SCALE_MUL>(p, src_slot, flat, s, stream);
-      case GS_SCALE_DIV: return pack_mode<SD, FD, GS_SCALE_DIV>(p, src_slot, flat, s, stream);
+      case GS_SCALE_NONE: return pack_mode<SD, FD, GS_SCALE_NONE, NT>(p, src_slot, flat, s, stream);
+      case GS_SCALE_MUL: return pack_mode<SD, FD, GS_SCALE_MUL, NT>(p, src_slot, flat, s, stream);
+      case GS_SCALE_DIV: return pack_mode<SD, FD, GS_SCALE_DIV, NT>(p, src_slot, flat, s, stream);
       default: return fail(GS_EINVAL, "gs_pack: unknown scale mode");
     }
   }));
   return GS_OK;
 }
 
+// the source grads are read once: non-temporal loads above the cache size (nt_read_once)
+int hip_pack(gs_plan* p, int src_slot, int src_dt, void* flat, int flat_dt, float s, int mode,
+             void* stream) {
+  DeviceGuard g(p->device);
+  return nt_read_once(p->elems * dtype_bytes(src_dt))
+             ? pack_nt<true>(p, src_slot, src_dt, flat, flat_dt, s, mode, stream)
+             : pack_nt<false>(p, src_slot, src_dt, flat, flat_dt, s, mode, stream);
+}
+
+// RED = 1: Σ dst² into sq (nullable); RED = 2: the non-finite flag, accumulated
+template <int RED, bool NT>
+static int unpack_nt(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* red, int acc,
+                     void* stream) {
+  GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
+    UnpackOp<GS_PACK_N, FD, DD, RED, NT> op;
+    op.want_red = red != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
+    return launch<GS_PACK_ILP>(p, op, stream, red, acc);
+  }));
+  return GS_OK;
+}
+
+// the flat buffer is read once: non-temporal loads above the cache size (nt_read_once)
 int hip_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* sq,
                int acc, void* stream) {
   DeviceGuard g(p->device);
-  GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
-    UnpackOp<GS_PACK_N, FD, DD, 1> op;
-    op.want_red = sq != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
-    return launch<GS_PACK_ILP>(p, op, stream, sq, acc);
-  }));
-  return GS_OK;
+  return nt_read_once(p->flat_numel * dtype_bytes(flat_dt))
+             ? unpack_nt<1, true>(p, flat, flat_dt, dst_slot, dst_dt, sq, acc, stream)
+             : unpack_nt<1, false>(p, flat, flat_dt, dst_slot, dst_dt, sq, acc, stream);
 }
 
 int hip_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found,
                      void* stream) {
   DeviceGuard g(p->device);
-  GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
-    UnpackOp<GS_PACK_N, FD, DD, 2> op;
-    op.want_red = true; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
-    // the flag accumulates (max), as torch's non-finite check does
-    return launch<GS_PACK_ILP>(p, op, stream, found, 1);
-  }));
-  return GS_OK;
+  // the flag accumulates (max), as torch's non-finite check does
+  return nt_read_once(p->flat_numel * dtype_bytes(flat_dt))
+             ? unpack_nt<2, true>(p, flat, flat_dt, dst_slot, dst_dt, found, 1, stream)
+             : unpack_nt<2, false>(p, flat, flat_dt, dst_slot, dst_dt, found, 1, stream);
 }
 
 int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
@@ -277,8 +293,9 @@ static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int group
 }
 // the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once)
 static int sqnorm_launch(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
-  return nt_read_once(p->elems * dtype_bytes(dt)) ? sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream)
-                                                  : sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
+  return nt_read_once(p->elems * dtype_bytes(dt), true)
+             ? sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream)
+             : sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
 }
 
 int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {

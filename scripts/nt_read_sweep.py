@@ -1,7 +1,8 @@
 """Σg² and the clip path under GS_NT_READ_ONCE (non-temporal loads of the read-once
 gradient stream: 0 never, 1 always, 2 when it is larger than the Infinity Cache,
 the default): Σg², Σg² partials, the clip path (partials + the clipped SGD) and
-the SGD alone, on ResNet-50's parameter shapes (102 MB of grads), ResNet-152's
+the SGD alone, and the bucket pack / unpack (the read-once source grads / flat
+buffer), on ResNet-50's parameter shapes (102 MB of grads), ResNet-152's
 (241 MB) and ResNet-152's x 2 (482 MB); plan launch timer (the kernels' own
 start / end).  One JSON line per row, with the Σg² value (scripts/r4q_nt_read.sh)."""
 import json
@@ -58,5 +59,23 @@ for model, reps in (("resnet50", 1), ("resnet152", 1), ("resnet152", 2)):
         if name == "sqnorm_f32":
             row["sqnorm"] = float(sq.item())
         print(json.dumps(row), flush=True)
-    del grads, ps, bufs, plan
+    bplan = TensorListPlan(numels, dev, align=64)
+    bplan.set_ptrs(1, grads)
+    flat = torch.randn(bplan.flat_numel, device=dev, generator=g) * 0.01
+    flat16 = torch.zeros(bplan.flat_numel, device=dev, dtype=torch.bfloat16)
+    for name, nbytes, fn in (("pack_f32", 8 * n, lambda: bplan.pack(1, torch.float32, flat, 0.125, 1)),
+                             ("pack_f32_to_bf16", 6 * n, lambda: bplan.pack(1, torch.float32, flat16, 0.125, 1)),
+                             ("unpack_f32", 8 * n, lambda: bplan.unpack(flat, 1, torch.float32)),
+                             ("unpack_f32+sqnorm", 8 * n, lambda: bplan.unpack(flat, 1, torch.float32, sqnorm=sq))):
+        for _ in range(3):
+            fn()
+        bplan.timer_enable(128)
+        for _ in range(30):
+            fn()
+        ts = bplan.timer_read()
+        bplan.timer_enable(0)
+        ms = sum(ts) / 30
+        print(json.dumps({"GS_NT_READ_ONCE": pol, "model": model, "replicas": reps, "grad_MB": 4 * n / 1e6,
+                          "kernel": name, "avg_ms": ms, "frac": nbytes / (ms * 1e-3) / 1e9 / 8000.0}), flush=True)
+    del grads, ps, bufs, plan, bplan, flat, flat16
     torch.cuda.empty_cache()
