@@ -396,10 +396,31 @@ def _beyond_ic_roofline(kernel_rates, zero, args):
     Infinity Cache right after the unpack wrote the grads)."""
     if not kernel_rates or zero is not None or args.engine != "ddp" or "beyond_ic" not in kernel_rates:
         return {}
-    row = kernel_rates["beyond_ic"]["kernels"]["sgd_momentum_wd" if args.optimizer == "sgd" else "adam"]
+    sgd = args.optimizer == "sgd"
+    row = kernel_rates["beyond_ic"]["kernels"]["sgd_momentum_wd" if sgd else "adam"]
     return {"frac_beyond_ic": row["frac"], "beyond_ic": {
         "achieved": row["GBps"], "avg_launch_ms": row["avg_ms"], "algorithmic_bytes_per_launch": row["alg_bytes"],
-        "set": kernel_rates["beyond_ic"]["set"], "timing": "plan launch timer, grad_sync_kernels.beyond_ic"}}
+        "set": kernel_rates["beyond_ic"]["set"], "timing": "plan launch timer, grad_sync_kernels.beyond_ic",
+        "plain_stream_ceiling": _mix_ceiling("sgd3r2w" if sgd else "adam4r3w")}}
+
+
+def _mix_ceiling(mix):
+    """The best rate a plain float4 grid reached for the same read / write mix on
+    the same number of elements (scripts/micro/stream_mix.hip: no chunk map, no
+    descriptors; committed run), as a fraction of 8 TB/s: what this kernel's
+    beyond-cache fraction is read against."""
+    path = os.path.join(REPO, "profiles", "r4", "r4p_stream_mix_2.jsonl")
+    try:
+        with open(path) as f:
+            rows = [json.loads(ln) for ln in f if ln.strip()]
+    except (OSError, ValueError):
+        return None
+    best = max((r for r in rows if r["case"].startswith(mix)), key=lambda r: r["frac"], default=None)
+    if best is None:
+        return None
+    return {"frac": round(best["frac"], 4), "case": best["case"], "grid": best["grid"],
+            "source": "profiles/r4/r4p_stream_mix_2.jsonl (scripts/micro/stream_mix.hip, a plain float4 stream of "
+                      "the same mix, ResNet-152 x 2 elements, one MI355X; box-to-box spread a few %)"}
 
 
 def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):

@@ -111,6 +111,8 @@ def _check_line(d, n):
     b = k["beyond_ic"]
     assert set(b["kernels"]) == set(k["kernels"]) and b["params"] > 100_000_000
     assert abs(r["frac_beyond_ic"] - b["kernels"]["sgd_momentum_wd"]["frac"]) < 1e-12
+    # ... read against a plain float4 stream of the same 3R2W mix (committed probe run)
+    assert r["beyond_ic"]["plain_stream_ceiling"]["case"].startswith("sgd3r2w")
     if n == 1:  # configs[3]'s N>1 clip path at its N=8 shard, over the one-rank RCCL communicator
         z, zs = k["clip_path_zero_n8"], k["clip_path_zero_n8_scalar"]
         assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > 0 and z["kernels_ms"] > 0
