@@ -130,16 +130,25 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
 #endif
 constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 
-// A stream read once (the gradient in Σg²) takes non-temporal loads when it is
-// larger than the Infinity Cache: none of it can still be resident from its
-// producer, and the NT path streams faster (a plain read-only float4 sum beyond
-// the cache: 0.84-0.87 of 8 TB/s NT vs 0.72-0.76 cached, scripts/micro/stream_mix.hip,
-// profiles/r4/r4p_stream_mix_*.jsonl).  At or below the cache size the loads stay
-// cached: the grads were just written and are largely resident (NT cost the
-// ResNet-50 rows 2-10 %, r4b).  GS_NT_READ_ONCE=0 never, 1 always, 2 the size rule;
-// GS_NT_SQNORM overrides it for the Σg² kernels alone (A/B).
+// A stream read once takes non-temporal loads when it is larger than the
+// Infinity Cache: none of it can still be resident from its producer, and the NT
+// path streams faster (a plain read-only float4 sum beyond the cache: 0.84-0.87
+// of 8 TB/s NT vs 0.72-0.76 cached, scripts/micro/stream_mix.hip,
+// profiles/r4/r4p_stream_mix_*.jsonl).  At or below the cache size the pack's
+// source and the unpack's flat buffer stay cached: NT cost them 5-16 % there
+// (r4r).  The Σg² kernels follow the same size rule.  Below the cache size the
+// better choice depends on the producer: right after libgsync's unpack wrote the
+// grads with non-temporal stores, NT Σg² loads ran the clip path 0.72 -> 0.80 at
+// ResNet-50 (profiles/r4/r4s_chain.jsonl); inside configs[3]'s real ZeRO step,
+// after RCCL wrote the shard, they cost 10 % (12.9 -> 14.2 us, r4v), and on the
+// bench's resident grads 2-5 % (r4u).  The DDP clip chain has a better answer
+// than NT loads, the Σg² folded into the unpack (fuse_grad_norm_into).
+// GS_NT_READ_ONCE / GS_NT_SQNORM: 0 never, 1 always, 2 the size rule (A/B).
 #ifndef GS_NT_READ_ONCE_DEFAULT
 #define GS_NT_READ_ONCE_DEFAULT 2
+#endif
+#ifndef GS_NT_SQNORM_DEFAULT
+#define GS_NT_SQNORM_DEFAULT 2
 #endif
 inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
   static const int policy = [] {
@@ -148,7 +157,7 @@ inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
   }();
   static const int policy_sq = [] {
     const char* e = std::getenv("GS_NT_SQNORM");
-    return e ? std::atoi(e) : policy;
+    return e ? std::atoi(e) : GS_NT_SQNORM_DEFAULT;
   }();
   const int pol = sqnorm ? policy_sq : policy;
   return pol == 2 ? stream_bytes > kInfinityCacheBytes : pol != 0;

@@ -291,11 +291,23 @@ static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int group
   });
   return GS_OK;
 }
+// A non-temporal Σg² leaves the grads out of the caches: the update that follows
+// then loads them non-temporally too (grads_read cleared).  GS_NT_SQ_HOT=1 keeps
+// the update's cached grad loads after it (A/B).
+static bool nt_sq_keeps_hot() {
+  static const bool v = [] {
+    const char* e = std::getenv("GS_NT_SQ_HOT");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 // the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once)
 static int sqnorm_launch(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
-  return nt_read_once(p->elems * dtype_bytes(dt), true)
-             ? sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream)
-             : sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
+  if (!nt_read_once(p->elems * dtype_bytes(dt), true))
+    return sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
+  if (!nt_sq_keeps_hot()) p->grads_read = false;
+  return sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream);
 }
 
 int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {

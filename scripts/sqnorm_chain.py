@@ -1,7 +1,8 @@
 """Σg² where the clip path runs it: right after the grads were written (a bucket
 unpack into the grads, then the Σg² partials, then the clipped SGD), per kernel
 by the plan launch timer, under GS_NT_SQNORM (the Σg² kernels' load policy:
-0 cached, 1 non-temporal, 2 the size rule = default).  ResNet-50 / ResNet-152 /
+0 cached, 1 non-temporal, 2 the size rule = default; GS_NT_SQ_HOT=1: the SGD
+keeps cached grad loads after a non-temporal Σg², "/hot" in the label).  ResNet-50 / ResNet-152 /
 ResNet-152 x 2 parameter shapes, fp32.  One JSON line per kernel and size
 (scripts/r4s_sqnorm_chain.sh)."""
 import json
@@ -11,12 +12,11 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from distributed_training_amd import _lib as L  # noqa: E402
 from distributed_training_amd.multi_tensor import TensorListPlan, update_task_units  # noqa: E402
 from distributed_training_amd.resnet import MODELS  # noqa: E402
 
 dev = torch.device("cuda", 0)
-pol = os.environ.get("GS_NT_SQNORM", "default")
+pol = os.environ.get("GS_NT_SQNORM", "default") + ("/hot" if os.environ.get("GS_NT_SQ_HOT") == "1" else "")
 for model, reps in (("resnet50", 1), ("resnet152", 1), ("resnet152", 2)):
     with torch.device("meta"):
         m = MODELS[model](num_classes=1000)
@@ -47,11 +47,13 @@ for model, reps in (("resnet50", 1), ("resnet152", 1), ("resnet152", 2)):
     plan.timer_enable(128)
     for _ in range(30):
         step()
-    rows = {"unpack_f32": (bplan.timer_read(kind=L.GS_OP_UNPACK), 8 * n),
-            "sqnorm_partial_f32": (plan.timer_read(kind=L.GS_OP_SQNORM), 4 * n),
-            "clipped_sgd": (plan.timer_read(kind=L.GS_OP_SGD), 20 * n)}
+    upd = plan.timer_read()  # one read (it drains the ring); the launches alternate partials, SGD
+    rows = {"unpack_f32": (bplan.timer_read(), 8 * n),
+            "sqnorm_partial_f32": (upd[0::2], 4 * n),
+            "clipped_sgd": (upd[1::2], 20 * n)}
     bplan.timer_enable(0)
     plan.timer_enable(0)
+    rows["clip_path_total"] = ([a + b for a, b in zip(upd[0::2], upd[1::2])], 24 * n)
     for name, (ts, nbytes) in rows.items():
         ms = sum(ts) / len(ts)
         print(json.dumps({"GS_NT_SQNORM": pol, "model": model, "replicas": reps, "kernel": name, "launches": len(ts),
