@@ -899,6 +899,16 @@ int red_fuse_groups() {
   }();
   return v;
 }
+// updates on a capped grid of contiguous group ranges (GS_UPD_CONTIG=<grid>,
+// 0 = off: one group per workgroup); VERDICT r3's candidate for the SGD beyond
+// the cache, A/B only
+int upd_contig_grid() {
+  static const int v = [] {
+    const char* e = std::getenv("GS_UPD_CONTIG");
+    return e ? std::max(0, std::min(std::atoi(e), kGridLimit)) : 0;
+  }();
+  return v;
+}
 bool red_contiguous() {
   static const bool v = [] {
     const char* e = std::getenv("GS_RED_CONTIG");
@@ -1378,6 +1388,10 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     PlanArgs a = p->args();
     a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
+    if (!red && (Op::kKind == GS_OP_SGD || Op::kKind == GS_OP_ADAM) && upd_contig_grid() > 0) {
+      grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, upd_contig_grid())));
+      a.per_wg = static_cast<int32_t>((groups + grid - 1) / grid);
+    }
     a.red_out = Op::kRed != 0 ? red_out : nullptr;  // groups_only: the contiguous group sums (nullable)
     a.red_acc = accumulate;
     a.red_fuse = fused ? red_fuse_groups() : 0;
