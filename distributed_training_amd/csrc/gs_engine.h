@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -720,6 +721,28 @@ __device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P,
   op.template apply<false>(v, local, 0u, f, acc);
 }
 
+// Stream-major issue (GS_STREAM_MAJOR=1, ops that expose kStreams / load_s<F, S>):
+// the G accesses of stream 0, then of stream 1, ... instead of every stream of
+// access 0, then of access 1 (scripts/micro/stream_mix.hip: +0.5-1.4 % on a plain
+// 3R2W stream at G = 4, profiles/r4/r4z_stream_mix.jsonl)
+#ifndef GS_STREAM_MAJOR
+#define GS_STREAM_MAJOR 0
+#endif
+template <class Op, class = void>
+struct op_streams { static constexpr int value = 0; };
+template <class Op>
+struct op_streams<Op, std::void_t<decltype(Op::kStreams)>> { static constexpr int value = Op::kStreams; };
+
+template <int S, int G, class Op>
+__device__ __forceinline__ void load_streams(const Op& op, const TV& v, int64_t e0, uint32_t tid,
+                                             typename Op::Frag (&f)[G]) {
+  if constexpr (S < op_streams<Op>::value) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) op.template load_s<true, S>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
+    load_streams<S + 1, G>(op, v, e0, tid, f);
+  }
+}
+
 template <int G, class Op>
 __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int t, int64_t c0, float& acc) {
   // G chunks c0 .. c0+G-1, all inside tensor t
@@ -728,8 +751,12 @@ __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int 
   const uint32_t tid = threadIdx.x;
   typename Op::Frag f[G];
   if (op.fast_ok(v)) {
+    if constexpr (GS_STREAM_MAJOR != 0 && op_streams<Op>::value > 0) {
+      load_streams<0, G>(op, v, e0, tid, f);
+    } else {
 #pragma unroll
-    for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
+      for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
+    }
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template apply<true>(v, e0, j * kChunkElems + tid * kUnit, f[j], acc);
   } else {
@@ -1173,6 +1200,14 @@ struct SgdOp {
     ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
     if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
+  // one stream of load() (stream-major issue, chunk_full)
+  static constexpr int kStreams = 3;
+  template <bool F, int S>
+  __device__ void load_s(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    if constexpr (S == 0) ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    else if constexpr (S == 1) ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
+    else if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+  }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
 #pragma unroll
@@ -1226,6 +1261,15 @@ struct AdamOp {
     ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
     ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
     ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+  }
+  // one stream of load() (stream-major issue, chunk_full)
+  static constexpr int kStreams = 4;
+  template <bool F, int S>
+  __device__ void load_s(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
+    if constexpr (S == 0) ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    else if constexpr (S == 1) ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
+    else if constexpr (S == 2) ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    else ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }
   template <bool F>
   __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {

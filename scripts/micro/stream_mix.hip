@@ -26,8 +26,10 @@ __device__ __forceinline__ void st(f4* p, f4 v) {
   else *p = v;
 }
 
-// R streams read (s[0..R-1]); the first W of them written back in place
-template <int R, int W, int G, bool NTL, bool NTS>
+// R streams read (s[0..R-1]); the first W of them written back in place.
+// SM: issue the loads stream-major (all G accesses of stream 0, then stream 1, ...)
+// instead of access-major (every stream of access 0, then access 1, ...)
+template <int R, int W, int G, bool NTL, bool NTS, bool SM = false>
 __global__ void __launch_bounds__(256) mix(f4* __restrict__ s0, f4* __restrict__ s1, f4* __restrict__ s2,
                                           f4* __restrict__ s3, int64_t n4, float* __restrict__ part) {
   f4* s[4] = {s0, s1, s2, s3};
@@ -35,11 +37,22 @@ __global__ void __launch_bounds__(256) mix(f4* __restrict__ s0, f4* __restrict__
   float acc = 0.f;
   for (int64_t base = (int64_t)blockIdx.x * 256 * G; base < n4; base += step) {
     f4 v[G][R];
+    if constexpr (SM) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int64_t i = base + (int64_t)g * 256 + threadIdx.x;
+      for (int r = 0; r < R; ++r) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[g][r] = i < n4 ? ld<NTL>(s[r] + i) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < G; ++g) {
+          const int64_t i = base + (int64_t)g * 256 + threadIdx.x;
+          v[g][r] = i < n4 ? ld<NTL>(s[r] + i) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int64_t i = base + (int64_t)g * 256 + threadIdx.x;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[g][r] = i < n4 ? ld<NTL>(s[r] + i) : f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -113,9 +126,10 @@ int main() {
   for (int round = 0; round < 2; ++round) {
     for (int gridc : {0, 2048, 8192}) {
       auto g_of = [&](int G) { return gridc ? gridc : (int)std::min<int64_t>(1 << 30, (n4 + 256 * G - 1) / (256 * G)); };
-#define CASE(NAME, BPE, R, W, G, NTL, NTS)                                                                      \
-  cs.push_back({NAME, BPE,                                                                                      \
-                time_ms([&] { mix<R, W, G, NTL, NTS><<<g_of(G), 256>>>(s[0], s[1], s[2], s[3], n4, part); }, 20), \
+#define CASE(NAME, BPE, R, W, G, NTL, NTS, ...)                                                                      \
+  cs.push_back({NAME, BPE,                                                                                           \
+                time_ms([&] { mix<R, W, G, NTL, NTS, ##__VA_ARGS__><<<g_of(G), 256>>>(s[0], s[1], s[2], s[3], n4, part); }, \
+                        20),                                                                                         \
                 gridc})
       CASE("read_sum_g4", 4, 1, 0, 4, false, true);
       CASE("read_sum_g4_ntl", 4, 1, 0, 4, true, true);
@@ -129,6 +143,9 @@ int main() {
       CASE("sgd3r2w_g8", 20, 3, 2, 8, false, true);
       CASE("adam4r3w_g4", 28, 4, 3, 4, false, true);
       CASE("adam4r3w_g4_ntl", 28, 4, 3, 4, true, true);
+      CASE("sgd3r2w_g4_ntl_streammajor", 20, 3, 2, 4, true, true, true);
+      CASE("sgd3r2w_g2_ntl_streammajor", 20, 3, 2, 2, true, true, true);
+      CASE("adam4r3w_g4_ntl_streammajor", 28, 4, 3, 4, true, true, true);
 #undef CASE
     }
   }

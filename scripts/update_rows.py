@@ -1,6 +1,7 @@
 """The fused SGD and Adam back to back at ResNet-50 and ResNet-152 x 2 sizes
-(plan launch timer), labelled with this process's GS_UPD_CONTIG (the update
-grid: one group per workgroup, or a capped grid of contiguous group ranges).
+(plan launch timer), labelled with this process's ROWS_LABEL (a library
+variant) or GS_UPD_CONTIG (the update grid: one group per workgroup, or a capped
+grid of contiguous group ranges).
 One JSON line per row (scripts/r4y_upd_contig.sh)."""
 import json
 import os
@@ -14,7 +15,7 @@ from distributed_training_amd.multi_tensor import TensorListPlan, update_task_un
 from distributed_training_amd.resnet import MODELS  # noqa: E402
 
 dev = torch.device("cuda", 0)
-label = os.environ.get("GS_UPD_CONTIG", "0")
+label = os.environ.get("ROWS_LABEL", os.environ.get("GS_UPD_CONTIG", "0"))
 with torch.device("meta"):
     r50 = [tuple(p.shape) for p in MODELS["resnet50"](num_classes=1000).parameters()]
 for setname, shapes in (("resnet50", r50), ("resnet152x2", bench._beyond_ic_shapes())):
@@ -35,7 +36,7 @@ for setname, shapes in (("resnet50", r50), ("resnet152x2", bench._beyond_ic_shap
         t = up.timer_read()
         up.timer_enable(0)
         ms = sum(t) / len(t)
-        print(json.dumps({"GS_UPD_CONTIG": label, "set": setname, "kernel": name, "avg_ms": ms,
-                          "frac": bpe * n / (ms * 1e-3) / 1e9 / 8000.0}), flush=True)
+        print(json.dumps({"GS_UPD_CONTIG": os.environ.get("GS_UPD_CONTIG", "0"), "variant": label, "set": setname,
+                          "kernel": name, "avg_ms": ms, "frac": bpe * n / (ms * 1e-3) / 1e9 / 8000.0}), flush=True)
     del ts, up
     torch.cuda.empty_cache()
