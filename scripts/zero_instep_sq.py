@@ -2,7 +2,7 @@
 ZeroDataParallel (stage 2, AdamW betas (0.8, 0.999), wd 3e-7, clip 1.0, one
 5e7-element bucket), one-rank RCCL; the shard plan's kernels (Σg² partials,
 then the clipped AdamW) timed by the plan launch timer inside real steps, under
-the GS_NT_SQNORM of this process.  One JSON line (scripts/r4v_zero_instep.sh)."""
+the GS_NT_SQNORM / GS_RED_GRID of this process.  One JSON line (scripts/r4v_zero_instep.sh)."""
 import json
 import os
 import sys
@@ -47,7 +47,8 @@ ts = zero.plan.timer_read()
 zero.plan.timer_enable(0)
 sq, upd = ts[0::2], ts[1::2]
 n = sum(zero.shard_sizes)
-print(json.dumps({"GS_NT_SQNORM": os.environ.get("GS_NT_SQNORM", "default"), "shard_elems": n,
+print(json.dumps({"GS_NT_SQNORM": os.environ.get("GS_NT_SQNORM", "default"),
+                  "GS_RED_GRID": os.environ.get("GS_RED_GRID", "default"), "shard_elems": n,
                   "sqnorm_partial_us": 1e3 * sum(sq) / len(sq), "adamw_us": 1e3 * sum(upd) / len(upd),
                   "sqnorm_frac": 2 * n / (sum(sq) / len(sq) * 1e-3) / 1e9 / 8000.0,
                   "adamw_frac": 28 * n / (sum(upd) / len(upd) * 1e-3) / 1e9 / 8000.0}), flush=True)
