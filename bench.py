@@ -108,13 +108,13 @@ def parse():
                          "curve at N>1 (distributed_training_amd.ddp.xgmi_bucket_caps)")
     ap.add_argument("--last-bucket-cap-mb", type=float, default=None,
                     help="cap the last bucket in gradient-ready order (the exposed end-of-backward chain)")
-    ap.add_argument("--zero-leg", type=int, default=-1,
+    ap.add_argument("--zero-leg", type=int, default=1,
                     help="after the headline: BASELINE configs[3] (ZeRO-2, bf16 ResNet-50) timed on the same "
-                         "ranks, reported as the line's `zero2` object (-1: at N > 1 on the DDP engine)")
-    ap.add_argument("--colossal-leg", type=int, default=-1,
+                         "ranks, reported as the line's `zero2` object (DDP engine; 0: off)")
+    ap.add_argument("--colossal-leg", type=int, default=1,
                     help="after the headline: BASELINE configs[4] (Colossal shim, ResNet-152 fp32 grads, fp16 "
                          "autocast, HybridAdam, 128 img/GPU) on the same ranks, the line's `colossal` object "
-                         "(-1: at N > 1 on the DDP engine)")
+                         "(DDP engine; 0: off)")
     ap.add_argument("--wall-budget-s", type=float, default=540.0,
                     help="whole-run wall budget from process start (warm-up compiles included): an optional leg "
                          "after the timed region runs only if its cost estimate (LEG_COST_S, measured) fits what "
@@ -307,7 +307,7 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     plan = TensorListPlan([shard], dev, task_units=update_task_units(dev))
     for k, t in enumerate((master, grads, m, v, p16)):
         plan.set_ptrs(k, [t])
-    groups = torch.zeros(L.GS_RED_GROUPS, device=dev)
+    groups = torch.zeros(L.GS_RED_PARTIALS, device=dev)
     sq = torch.zeros(1, device=dev)
     out = torch.zeros(3, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -315,10 +315,10 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     def adam():
         plan.adam(torch.bfloat16, 1e-3, 0.8, 0.999, 1e-8, 3e-7, True, False, -1e-3, 0.5, lowp_dtype=torch.bfloat16)
 
-    def folded():
-        n = plan.sqnorm_partial_out(1, torch.bfloat16, groups)
-        comm.all_reduce(groups[:n], stream=stream)
-        plan.set_clip_groups(1.0, 1e-6, groups, n, out=out)
+    def folded():  # as zero.py: the whole partial-sum buffer travels and is folded
+        plan.sqnorm_partial_out(1, torch.bfloat16, groups)
+        comm.all_reduce(groups, stream=stream)
+        plan.set_clip_groups(1.0, 1e-6, groups, groups.numel(), out=out)
         adam()
 
     def scalar():
@@ -362,12 +362,15 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
         for _ in range(iters):
             fn()
         torch.cuda.synchronize()
-        kern = plan.timer_read()
+        kern = plan.timer_read_by_kind()
         plan.timer_enable(0)
         nbytes = 30 * shard
+        sq_ms = sum(kern.get(L.GS_OP_SQNORM, [])) / iters
+        up_ms = sum(kern.get(L.GS_OP_ADAM, [])) / iters
         rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9,
                       "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "shard_elems": shard,
-                      "kernels_ms": sum(kern) / iters, "host_paced_ms": host_ms,
+                      "kernels_ms": sq_ms + up_ms, "sqnorm_kernel_ms": sq_ms, "update_kernel_ms": up_ms,
+                      "host_paced_ms": host_ms,
                       "timing": ("HIP events around the call, the stream pre-loaded by a spin kernel (the launches "
                                  "queued ahead, as behind backward)" if spin else "HIP events around the call"),
                       "launches": ("sqnorm_partial_out + all_reduce(<=64 floats) + clipped AdamW"
@@ -389,19 +392,51 @@ def _beyond_ic_shapes():
     return [tuple(p.shape) for p in m.parameters()] * 2
 
 
-def _beyond_ic_roofline(kernel_rates, zero, args):
+def _beyond_ic_roofline(kernel_rates, zero, args, traffic_json):
     """The headline update kernel's true-HBM rate, measured in this run: the same
-    kernel on the >256 MiB working set of grad_sync_kernel_rates (the in-step
-    `frac` runs on ResNet-50's 511 MB read/write set, partly served by the 256 MiB
-    Infinity Cache right after the unpack wrote the grads)."""
+    kernel on the >256 MiB working set of grad_sync_kernel_rates (ResNet-152
+    shapes x 2: 2.41 GB per SGD launch).  The in-step figure runs on ResNet-50's
+    511 MB read/write set, partly served by the 256 MiB Infinity Cache right after
+    the unpack wrote the grads (it reads above the measured copy ceiling), so the
+    line's headline `frac` is this one; {} when the rows were
+    not measured (the in-step figure then stays the headline, flagged)."""
     if not kernel_rates or zero is not None or args.engine != "ddp" or "beyond_ic" not in kernel_rates:
         return {}
     sgd = args.optimizer == "sgd"
     row = kernel_rates["beyond_ic"]["kernels"]["sgd_momentum_wd" if sgd else "adam"]
-    return {"frac_beyond_ic": row["frac"], "beyond_ic": {
-        "achieved": row["GBps"], "avg_launch_ms": row["avg_ms"], "algorithmic_bytes_per_launch": row["alg_bytes"],
-        "set": kernel_rates["beyond_ic"]["set"], "timing": "plan launch timer, grad_sync_kernels.beyond_ic",
-        "plain_stream_ceiling": _mix_ceiling("sgd3r2w" if sgd else "adam4r3w")}}
+    traffic = None
+    try:
+        with open(traffic_json) as f:
+            traffic = json.load(f).get(f"resnet152x2/{args.optimizer}", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    out = {"achieved": row["GBps"], "frac": row["frac"], "avg_launch_ms": row["avg_ms"],
+           "algorithmic_bytes_per_launch": row["alg_bytes"], "launches": kernel_rates.get("iters"),
+           "traffic": traffic, "set": kernel_rates["beyond_ic"]["set"],
+           "timing": "plan launch timer (hipExtLaunchKernel's events: the kernel's own start / end), "
+                     "grad_sync_kernels.beyond_ic, after the timed region, back-to-back launches",
+           "plain_stream_ceiling": _mix_ceiling("sgd3r2w" if sgd else "adam4r3w")}
+    trace = _trace_check("SgdOp_beyond_ic" if sgd else "AdamOp_beyond_ic", row["alg_bytes"])
+    if trace:
+        out["rocprof"] = trace
+    return out
+
+
+def _trace_check(key, alg_bytes):
+    """The same launches' average duration in the committed rocprofv3 kernel trace
+    of the driver's command (profiles/trace_roofline.json, scripts/trace_bench.py)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "trace_roofline.json")) as f:
+            tr = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+    if not tr:
+        return None
+    return {"kernel_trace_avg_ms": tr["avg_us"] * 1e-3, "launches": tr.get("timed_region_launches"),
+            "frac_at_trace_duration": alg_bytes / (tr["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBPS,
+            "source": "profiles/trace_roofline.json: rocprofv3 --kernel-trace of this command on a committed run "
+                      f"({tr.get('run', 'see DESIGN §5')}); the profiler's per-kernel completion handling adds a "
+                      "few µs, box-to-box spread ±4 %"}
 
 
 def _mix_ceiling(mix):
@@ -433,7 +468,7 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
     n, rows = _kernel_rows([tuple(p.shape) for p in params], dev, iters)
     n_big, big = _kernel_rows(_beyond_ic_shapes(), dev, iters)
     torch.cuda.empty_cache()
-    out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS,
+    out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS, "iters": iters,
            "timing": "after the timed region, warm, alone on the GPU; plan launch timer (the kernels' own start "
                      "and end: hipExtLaunchKernel's HIP events on the launch stream; GS_TIMER_EXT=0 = an event "
                      f"pair around the launch), average of {iters} calls",
@@ -484,13 +519,14 @@ def _engine_comm(ddp, zero):
 
 
 # Cost estimates of the optional legs after the timed region (seconds), for the
-# --wall-budget-s skip decision: the larger of the N=1 run with every leg forced on
-# (profiles/r3/r3n_bench_n1_all_legs.json leg_seconds) and the 4-rank full-size
-# rehearsals (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json,
-# profiles/r4/r4d_n4_budget240.json), doubled,
-# and at least 5 s; zero2 / colossal include their first-step MIOpen compiles.
+# --wall-budget-s skip decision: the larger of the N=1 runs with every leg on
+# (profiles/r3/r3n_bench_n1_all_legs.json; profiles/r5/r5a_bench_legs_n1.json: zero2
+# 1.2 s, colossal 35.3 s) and the 4-rank full-size rehearsals
+# (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json,
+# profiles/r4/r4d_n4_budget240.json), doubled, and at least 5 s; zero2 / colossal
+# include their first-step MIOpen compiles; the policy A/B has 8 variants since r5.
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
-              "zero2": 2 * 18.4, "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 35.0}
+              "zero2": 2 * 18.4, "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 35.0 * 8 / 6}
 # the reference's DeepSpeed optimizer (R:resnet/deepspeed/deepspeed_train.py:175-186): "Adam" in
 # AdamW mode, betas (0.8, 0.999), eps 1e-8, weight_decay 3e-7; gradient_clipping 1.0 (:195)
 DS_ADAM = dict(lr=1e-3, betas=(0.8, 0.999), eps=1e-8, weight_decay=3e-7)
@@ -515,10 +551,15 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     bucket_dtype = torch.bfloat16 if args.bucket_dtype == "bf16" else None
     # bf16_buckets: half the bytes on the links, but other numerics (opt-in) — reported,
     # never a candidate for the default
+    # gradient_as_bucket_view (no unpack: the grads are bucket views) and the overlapped
+    # optimizer (each bucket's update behind its unpack, under backward) shorten the
+    # exposed tail with the numerics unchanged: candidates like the layouts
     variants = [("torch", {}), ("xgmi", {"bucket_policy": "xgmi"}),
                 ("last_bucket_cap_1MiB", {"last_bucket_cap_mb": 1.0}),
                 *([("bf16_buckets", {"bucket_dtype": torch.bfloat16})] if bucket_dtype is None else []),
                 ("rccl_cta_cap_16", {"rccl_max_ctas": 16}),
+                ("grad_as_bucket_view", {"gradient_as_bucket_view": True}),
+                ("optimizer_overlap", {"optimizer_overlap": True}),
                 ("torch_again", {})]
     ddp.close()
     peak = (world - 1) * XGMI_LINK_GBPS
@@ -526,12 +567,21 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
     for name, kw in variants:
         kw = dict(kw)
         bdt = kw.pop("bucket_dtype", bucket_dtype)
+        gview = kw.pop("gradient_as_bucket_view", args.grad_as_bucket_view)
+        overlap = kw.pop("optimizer_overlap", False)
         try:
             v = D.DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, bucket_dtype=bdt,
-                                          gradient_as_bucket_view=args.grad_as_bucket_view, **kw)
+                                          gradient_as_bucket_view=gview, **kw)
         except Exception as e:  # e.g. RCCL refusing a communicator config: every rank alike
             rows[name] = {"error": f"{type(e).__name__}: {e}"[:300], "parity": None}
             continue
+        vopt = opt
+        if overlap:
+            if args.optimizer == "sgd":
+                v._register_fused_optim(torch.optim.SGD, lr=0.1, momentum=0.9, weight_decay=1e-4)
+            else:
+                v._register_fused_optim(torch.optim.Adam, lr=1e-3 * world)
+            vopt = _OverlappedStep(v)
 
         def fwd_bwd():
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -540,8 +590,8 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
 
         def one():
             fwd_bwd()
-            opt.step()
-            opt.zero_grad(set_to_none=True)
+            vopt.step()
+            vopt.zero_grad(set_to_none=True)
 
         for _ in range(2):
             one()
@@ -577,14 +627,14 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
         cal = v._get_ddp_logging_data().get("xgmi_calibration")
         if cal:
             row["xgmi_calibration"] = cal
-        row["parity"] = PC.ddp_parity_step(v, opt, fwd_bwd)
+        row["parity"] = PC.ddp_parity_step(v, vopt, fwd_bwd)
         rows[name] = row
         v.close()
     base = (rows["torch"]["images_per_sec"] + rows["torch_again"]["images_per_sec"]) / 2
     best, best_ips = "torch", base * (1 + POLICY_MARGIN)
     if "images_per_sec" in rows.get("bf16_buckets", {}):
         rows["bf16_buckets"]["vs_torch"] = rows["bf16_buckets"]["images_per_sec"] / base
-    for name in ("xgmi", "last_bucket_cap_1MiB", "rccl_cta_cap_16"):
+    for name in ("xgmi", "last_bucket_cap_1MiB", "rccl_cta_cap_16", "grad_as_bucket_view", "optimizer_overlap"):
         r = rows[name]
         if "error" in r:
             continue
@@ -598,16 +648,11 @@ def bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args, steps=8):
             "decision": best}
 
 
-def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
-    """BASELINE configs[3] inside the N > 1 run: a fresh ResNet-50 in bf16 on the
-    libgsync ZeRO-2 engine as the DeepSpeed config drives it
-    (R:resnet/deepspeed/deepspeed_train.py:170-219: bf16, stage 2, AdamW,
-    gradient_clipping 1.0, reduce_bucket_size 5e7; reduce-scatter of bf16
-    grads, fp32 master shard update, all-gather of bf16 params) on the same
-    communicator, `steps` timed steps (MAX over ranks) and one self-checked
-    step.  The headline line is the DDP engine; this object is configs[3] at
-    the same N."""
-    import distributed_training_amd as D  # noqa: F401
+def _zero2_run(args, world, rank, dev, coll_h, steps, warmup, overlap_allgather=False):
+    """One configs[3] engine on a fresh bf16 ResNet-50: `steps` timed steps (MAX
+    over ranks), the shard update's launches, the end-of-step all-gather timed on
+    one more step (HIP events around it on the step's stream: its exposed time),
+    and the self-checked parity step."""
     from distributed_training_amd import _lib as L
     from distributed_training_amd import parity as PC
     from distributed_training_amd.resnet import MODELS
@@ -616,7 +661,7 @@ def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
     torch.manual_seed(0)
     model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
     zero = ZeroDataParallel(model, stage=2, optimizer="adamw", momentum=0.9, reduce_bucket_size=int(5e7),
-                            gradient_clipping=1.0, **DS_ADAM)
+                            gradient_clipping=1.0, overlap_allgather=overlap_allgather, **DS_ADAM)
     g = torch.Generator(device=dev).manual_seed(4321 + rank)
     x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
     x = x.to(torch.bfloat16)
@@ -644,19 +689,45 @@ def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
     el = coll_h.max(time.perf_counter() - t0)
     upd = zero.plan.timer_read(kind=L.GS_OP_ADAM)
     zero.plan.timer_enable(0)
-    shard = sum(p.numel() for p in zero.params) // world
+    zero.time_allgather(True)
+    one()
+    ag_ms = zero.last_allgather_ms()
+    zero.time_allgather(False)
+    shard = sum(zero.shard_sizes)
     upd_ms = sum(upd) / len(upd) if upd else None
-    out = {"engine": "zero2", "config": "BASELINE configs[3]: ResNet-50 bf16 model, ZeRO-2 reduce-scatter + "
-                                        "AdamW on fp32 master shards + all-gather, clip 1.0",
-           "optimizer": dict(DS_ADAM, kind="adamw", gradient_clipping=1.0),
-           "images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3,
-           "per_gpu_batch": args.batch, "steps": steps, "warmup": warmup,
+    out = {"images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3,
+           "per_gpu_batch": args.batch, "steps": steps, "warmup": warmup, "buckets": len(zero.buckets),
            "shard_update": {"avg_launch_ms": upd_ms, "alg_bytes_per_launch": 28 * shard,
-                            "frac": 28 * shard / (upd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if upd_ms else None}}
+                            "frac": 28 * shard / (upd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if upd_ms else None},
+           "allgather_exposed_ms": ag_ms,
+           "allgather_timing": ("HIP events around the end-of-step all-gathers on the step's stream, one step "
+                                "after the timed region" + ("; overlap_allgather: their issue only, the gathers "
+                                                            "run on the communicator's stream under the next "
+                                                            "forward" if overlap_allgather else ""))}
+    zero.wait_allgather()
     out["parity"] = PC.zero_parity_step(zero, fwd_bwd)
     zero.close()
     del zero, model
     torch.cuda.empty_cache()
+    return out
+
+
+def zero2_leg(args, world, rank, dev, coll_h, steps=8, warmup=3):
+    """BASELINE configs[3] on the same ranks as the headline: a fresh ResNet-50
+    in bf16 on the libgsync ZeRO-2 engine as the DeepSpeed config drives it
+    (R:resnet/deepspeed/deepspeed_train.py:170-219: bf16, stage 2, AdamW,
+    gradient_clipping 1.0, reduce_bucket_size 5e7; reduce-scatter of bf16
+    grads, fp32 master shard update, all-gather of bf16 params) on the same
+    communicator, `steps` timed steps (MAX over ranks) and one self-checked
+    step.  At N > 1 also the opt-in overlapped all-gather (ZeroDataParallel
+    overlap_allgather: per-bucket gathers under the next forward), timed and
+    parity-checked the same way."""
+    out = {"engine": "zero2", "config": "BASELINE configs[3]: ResNet-50 bf16 model, ZeRO-2 reduce-scatter + "
+                                        "AdamW on fp32 master shards + all-gather, clip 1.0",
+           "optimizer": dict(DS_ADAM, kind="adamw", gradient_clipping=1.0)}
+    out.update(_zero2_run(args, world, rank, dev, coll_h, steps, warmup))
+    if world > 1:
+        out["overlap_allgather"] = _zero2_run(args, world, rank, dev, coll_h, steps, warmup, overlap_allgather=True)
     return out
 
 
@@ -694,18 +765,32 @@ def colossal_leg(args, world, rank, dev, coll_h, batch=128, steps=8, warmup=3):
     for _ in range(warmup):
         one()
     torch.cuda.synchronize()
+    opt.enable_kernel_timer(steps + 4)  # HybridAdam = libgsync FusedAdam: its update launches
+    flags = []
     coll_h.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
+        flags.append(opt_w.scaler._state(opt_w.optim)["found_inf"].clone())  # device copy, no sync
     torch.cuda.synchronize()
     coll_h.barrier()
     el = coll_h.max(time.perf_counter() - t0)
+    n_params = sum(p.numel() for p in ddp._params)
+    # fp16 GradScaler: an overflowing step's update exits at once on the device flag;
+    # only the launches that updated count toward the rate (as the colossal engine's headline)
+    ms = opt.kernel_ms()
+    upd = [m for m, f in zip(ms, flags) if f.item() == 0] if len(ms) == len(flags) else ms
+    opt.enable_kernel_timer(0)
+    upd_ms = sum(upd) / len(upd) if upd else None
     out = {"engine": "colossal", "model": name,
            "config": "BASELINE configs[4]: ResNet-152 fp32 params/grads through the Colossal "
                      "Booster(TorchDDPPlugin, fp16) + HybridAdam, libgsync DDP underneath",
            "images_per_sec": world * batch * steps / el, "ms_per_step": el / steps * 1e3, "per_gpu_batch": batch,
-           "steps": steps, "warmup": warmup, "grad_bytes_per_step": 4 * sum(p.numel() for p in ddp._params)}
+           "steps": steps, "warmup": warmup, "grad_bytes_per_step": 4 * n_params,
+           "fused_adam": {"avg_launch_ms": upd_ms, "alg_bytes_per_launch": 28 * n_params,
+                          "frac": 28 * n_params / (upd_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if upd_ms else None,
+                          "launches": len(upd), "skipped_launches": len(ms) - len(upd),
+                          "timing": "libgsync plan launch timer (the kernel's own start / end), the timed steps"}}
     out["parity"] = PC.ddp_parity_step(ddp, opt_w, fwd_bwd)
     opt_w.zero_grad()
     ddp.close()
@@ -1029,23 +1114,11 @@ def main():
         except Exception:
             traffic = None
     # the same launches' kernel durations from the committed rocprofv3 kernel trace of
-    # this command (scripts/gpu_round.sh PROFILE=1 -> scripts/trace_roofline.py)
+    # this command (scripts/trace_bench.py)
     trace_check = None
-    trace_json = os.path.join(REPO, "profiles", "trace_roofline.json")
-    if (os.path.exists(trace_json) and zero is None and args.impl == "libgsync" and args.engine == "ddp"
-            and args.model == "resnet50" and args.optimizer == "sgd" and not args.graph):
-        try:
-            with open(trace_json) as f:
-                tr = json.load(f).get("SgdOp")
-            if tr:
-                trace_check = {"kernel_trace_avg_ms": tr["avg_us"] * 1e-3,
-                               "frac_at_trace_duration": bytes_per_param * upd_params / (tr["avg_us"] * 1e-6)
-                               / 1e9 / HBM_PEAK_GBPS,
-                               "source": "profiles/trace_roofline.json: rocprofv3 kernel trace of the timed "
-                                         "launches of this command on a committed run (the profiler's per-kernel "
-                                         "completion handling adds a few µs; box-to-box spread ±4 %)"}
-        except Exception:
-            trace_check = None
+    if (zero is None and args.impl == "libgsync" and args.engine == "ddp" and args.model == "resnet50"
+            and not args.graph):
+        trace_check = _trace_check("SgdOp" if args.optimizer == "sgd" else "AdamOp", bytes_per_param * upd_params)
     if torch_zero:
         log = {"has_rebuilt_buckets": 0}
         bucket_bytes = []
@@ -1058,6 +1131,55 @@ def main():
     else:
         log = {"has_rebuilt_buckets": 0}
         bucket_bytes = [b.numel() * b.element_size() for b in zero.grad_bufs]
+
+    def _roofline():
+        kernel = ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
+                  if args.engine == "colossal" else
+                  f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update "
+                  f"(chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
+                  if zero is None else
+                  f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> "
+                  f"+ bf16 param write)")
+        in_step = {
+            "achieved": achieved,
+            "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+            "frac_of_copy_ceiling": achieved / HBM_COPY_GBPS if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
+            "avg_launch_ms": opt_ms_avg,
+            "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
+            "launches": len(opt_ms),
+            "timing": ("libgsync plan launch timer: the kernel's own start / end, hipExtLaunchKernel's HIP events "
+                       "on the launch stream, the timed steps' launches"
+                       + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
+                       + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
+                          if args.optimizer_overlap else "")),
+            **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
+            **({"rocprof": trace_check} if trace_check else {}),
+        }
+        # reads above the copy ceiling come partly from the 256 MiB Infinity Cache
+        in_step["ic_assisted"] = bool(achieved and achieved > HBM_COPY_GBPS)
+        bic = _beyond_ic_roofline(kernel_rates, zero, args, args.traffic_json)
+        head = bic if bic else in_step
+        r = {"kernel": kernel, "bound": "hbm", "achieved": head["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+             "frac": head["frac"], "traffic": head["traffic"],
+             "algorithmic_bytes_per_launch": head["algorithmic_bytes_per_launch"],
+             "avg_launch_ms": head["avg_launch_ms"], "launches": head["launches"],
+             "copy_ceiling": HBM_COPY_GBPS,
+             "frac_of_copy_ceiling": head["achieved"] / HBM_COPY_GBPS if head["achieved"] else None,
+             "working_set": (f"beyond the Infinity Cache: {bic['set']}, {bic['algorithmic_bytes_per_launch'] / 1e9:.2f} "
+                             "GB per launch (true HBM)") if bic else
+                            f"in the training step ({args.model}; ic_assisted = {in_step['ic_assisted']})",
+             "timing": head["timing"]}
+        if bic:
+            r["frac_beyond_ic"] = bic["frac"]
+            r["plain_stream_ceiling"] = bic["plain_stream_ceiling"]
+            if "rocprof" in bic:
+                r["rocprof"] = bic["rocprof"]
+            r["in_step"] = in_step
+        else:
+            r.update({k: v for k, v in in_step.items() if k not in r})
+        return r
 
     def make_line():
         grad_sync = {"bucket_bytes": bucket_bytes, "n_buckets": len(bucket_bytes), "grad_bytes_per_step": grad_bytes}
@@ -1135,35 +1257,7 @@ def main():
                    if args.pg_backend == "gloo" else {}),
                 "params": n_params,
             },
-            "roofline": None if args.impl == "torch" else {
-                "kernel": ("gs fused Adam update (chunk_kernel<AdamOp>, HybridAdam via the Colossal shim)"
-                           if args.engine == "colossal" else
-                           f"gs fused {'SGD' if args.optimizer == 'sgd' else 'Adam'} update "
-                           f"(chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}>)"
-                           if zero is None else
-                           f"gs ZeRO shard update (chunk_kernel<{'SgdOp' if args.optimizer == 'sgd' else 'AdamOp'}> "
-                           f"+ bf16 param write)"),
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBPS if achieved else None,
-                "copy_ceiling": HBM_COPY_GBPS,
-                "frac_of_copy_ceiling": achieved / HBM_COPY_GBPS if achieved else None,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_per_param * upd_params,
-                "avg_launch_ms": opt_ms_avg,
-                "launches": len(opt_ms),
-                "timing": ("libgsync plan launch timer: the kernel's own start / end, hipExtLaunchKernel's HIP events "
-                           "on the launch stream (GS_TIMER_EXT=0: an event pair around the launch)"
-                           + ("; graph mode: 5 eager launches after the timed region" if args.graph else "")
-                           + ("; optimizer overlap: per step, the sum of the per-bucket launches (under backward)"
-                              if args.optimizer_overlap else "")),
-                "median_launch_ms": opt_ms[len(opt_ms) // 2] if opt_ms else None,
-                **({"skipped_launches": sum(f.item() != 0 for f in skip_flags)} if skip_flags else {}),
-                **({"rocprof": trace_check} if trace_check else {}),
-                **_beyond_ic_roofline(kernel_rates, zero, args),
-            },
+            "roofline": None if args.impl == "torch" else _roofline(),
             "grad_sync": grad_sync,
             "grad_sync_kernels": kernel_rates,
             "parity": parity,
@@ -1312,13 +1406,13 @@ def main():
             [p for p in model.parameters() if p.requires_grad] if zero is None else zero.params, dev,
             comm=_engine_comm(ddp, zero), world=world) if rank == 0 else None)
 
-    want_zero = args.zero_leg == 1 or (args.zero_leg == -1 and world > 1)
+    want_zero = args.zero_leg != 0
     if want_zero and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
         zero2 = leg("zero2", lambda: zero2_leg(args, world, rank, dev, coll_h))
         if rank == 0 and zero2 is not None:
             print(f"[bench] zero2 leg: {zero2['images_per_sec']:.1f} images/s, parity {zero2['parity'].get('ok')}",
                   file=sys.stderr, flush=True)
-    want_col = args.colossal_leg == 1 or (args.colossal_leg == -1 and world > 1)
+    want_col = args.colossal_leg != 0
     if want_col and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
         colossal = leg("colossal", lambda: colossal_leg(args, world, rank, dev, coll_h,
                                                         batch=min(128, args.batch)))

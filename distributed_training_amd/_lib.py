@@ -31,7 +31,8 @@ GS_DEV_HOST, GS_DEV_HIP = 0, 1
 GS_SUM, GS_PROD, GS_MAX, GS_MIN, GS_AVG = 0, 1, 2, 3, 4
 GS_SCALE_NONE, GS_SCALE_MUL, GS_SCALE_DIV = 0, 1, 2
 GS_PLAN_SLOTS = 5
-GS_RED_GROUPS = 64  # gs_sqnorm_partial_out: at most this many group sums
+GS_RED_GROUPS = 64  # the fused reduction's group sums (one per lane of the folding wave)
+GS_RED_PARTIALS = 512  # gs_sqnorm_partial_out: the caller's buffer, at most this many partial sums
 GS_BKT_AUTO_COLLECTIVE = 1
 GS_BKT_GRAD_VIEW = 2
 GS_BKT_NO_SCALE = 4
@@ -204,7 +205,11 @@ def available() -> bool:
         return False
 
 
-HOOK_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "_gshook.so")
+# the hooks beside the loaded library: lib/, or a variant directory holding its own
+# libgsync.so + _gshook.so (A/B runs; _gshook's rpath $ORIGIN resolves its libgsync there)
+HOOK_PATH = os.path.join(os.path.dirname(os.path.abspath(LIB_PATH)), "_gshook.so")
+if not os.path.exists(HOOK_PATH):
+    HOOK_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "_gshook.so")
 _hook_mod = None
 _hook_error: str | None = None
 
@@ -212,8 +217,8 @@ _hook_error: str | None = None
 def hook_module():
     """The _gshook extension (C++ DDP gradient hooks, csrc/gs_torch_hook.cpp),
     or None when it is not built — DDP then keeps its Python hooks, which call
-    the same library.  It links lib/libgsync.so itself, so a GSYNC_LIB variant
-    (a different library instance) disables it."""
+    the same library.  It links the libgsync.so of its own directory, so a
+    GSYNC_LIB variant without a _gshook.so beside it disables it."""
     global _hook_mod, _hook_error
     if _hook_mod is not None or _hook_error is not None:
         return _hook_mod

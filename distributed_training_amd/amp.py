@@ -15,6 +15,7 @@ keep torch's host read of the flag (T:amp/grad_scaler.py _maybe_opt_step).  Reac
 from __future__ import annotations
 
 import torch
+from torch.autograd.graph import increment_version
 
 from .multi_tensor import TensorListPlan
 
@@ -105,6 +106,10 @@ class GradScaler:
                 self._plans[key] = plan
             plan.set_ptrs(0, grads)
             plan.unscale_check(0, dt, st["inv_scale"] if unscale else None, st["found_inf"])
+            if unscale:
+                # grads multiplied in place by the kernel: bump their version counters
+                # as torch's in-place unscale does (a DDP's fused Σg² of them is stale)
+                increment_version(grads)
         return st
 
     def unscale_(self, optimizer):

@@ -58,10 +58,28 @@ struct Bucket {
   // timing (all on the comm stream but ev_ready, recorded on the producer):
   // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
-  hipEvent_t ev_sync = nullptr;  // untimed ready event (timeline level 0, or not the last bucket at level 1)
+  hipEvent_t ev_sync = nullptr;  // untimed ready event (a comm-stream chain waits on it)
   bool timed = false;            // pk0 / t0 / t1 / u1 recorded (level 2)
   bool ready_timed = false;      // ev_ready recorded
 };
+
+// Timing events ride on the chain's own kernels (hipExtLaunchKernel's start / stop,
+// written by the dispatch) instead of event packets of their own: a packet costs
+// ~4.7 µs of stream time on the exposed chain, an event carried by a launch ~2.4 µs
+// (scripts/micro/event_chain.hip, profiles/r5/r5a_event_chain.jsonl).  arm() hands
+// the events to the plan's next launch; settle() records whatever no launch took
+// (an empty plan, a grad-view bucket that needs no scaling) at that point instead.
+void arm(gs_plan* p, hipEvent_t start, hipEvent_t stop) {
+  p->once_start = start;
+  p->once_stop = stop;
+}
+int settle(gs_plan* p, hipStream_t s) {
+  hipEvent_t a = static_cast<hipEvent_t>(p->once_start), b = static_cast<hipEvent_t>(p->once_stop);
+  p->once_start = p->once_stop = nullptr;
+  if (a && hipEventRecord(a, s) != hipSuccess) return fail(GS_EHIP, "timeline event record failed");
+  if (b && hipEventRecord(b, s) != hipSuccess) return fail(GS_EHIP, "timeline event record failed");
+  return GS_OK;
+}
 
 }  // namespace
 
@@ -95,7 +113,9 @@ struct gs_bucketer {
   int timeline = 1;
   hipEvent_t ev_comm = nullptr;     // comm stream's earlier buckets, joined before a producer-side tail
   bool done_timed = false;
-  bool tail_on_producer = true;     // GSYNC_TAIL_ON_PRODUCER=0 keeps every bucket on the comm stream
+  hipEvent_t done_ev = nullptr;     // this iteration's "every chain done" mark: ev_done, or the stop
+                                    // event of the producer-side tail's last kernel (done_on_chain)
+  bool done_on_chain = false;
   bool tail_ran_on_producer = false;
   std::mutex mu;
 
@@ -131,20 +151,36 @@ int debug_sum(gs_bucketer* b, Bucket& bk, int which, void* stream) {
 }
 
 // after the collective: unpack into the grads (with the fused Σg² or the fused
-// non-finite check), or, when the grads ARE the bucket, just the check
-int unpack_one(gs_bucketer* b, Bucket& bk, void* stream, int accumulate_sq) {
+// non-finite check), or, when the grads ARE the bucket, just the check.  e0 / e1:
+// timing events carried by the first / last kernel of this step (nullable).
+int unpack_one(gs_bucketer* b, Bucket& bk, void* stream, int accumulate_sq, hipEvent_t e0 = nullptr,
+               hipEvent_t e1 = nullptr) {
   float* sq = b->sqnorm;
+  hipStream_t s = static_cast<hipStream_t>(stream);
   if (b->do_unpack()) {
     if (b->found_inf && !sq) {
+      arm(bk.plan, e0, e1);
       GS_TRY_RET(gs_unpack_check(bk.plan, bk.buf, bk.bdt, 1, bk.gdt, b->found_inf, stream));
+      GS_TRY_RET(settle(bk.plan, s));
     } else {
       const int acc = (b->sq_count > 0 || accumulate_sq) ? 1 : 0;
+      arm(bk.plan, e0, b->found_inf ? nullptr : e1);
       GS_TRY_RET(gs_unpack(bk.plan, bk.buf, bk.bdt, 1, bk.gdt, sq, acc, stream));
+      GS_TRY_RET(settle(bk.plan, s));
       if (sq) ++b->sq_count;
-      if (b->found_inf) GS_TRY_RET(gs_unscale_check(bk.flat, 0, bk.bdt, nullptr, b->found_inf, stream));
+      if (b->found_inf) {
+        arm(bk.flat, nullptr, e1);
+        GS_TRY_RET(gs_unscale_check(bk.flat, 0, bk.bdt, nullptr, b->found_inf, stream));
+        GS_TRY_RET(settle(bk.flat, s));
+      }
     }
   } else if (b->found_inf) {
+    arm(bk.flat, e0, e1);
     GS_TRY_RET(gs_unscale_check(bk.flat, 0, bk.bdt, nullptr, b->found_inf, stream));
+    GS_TRY_RET(settle(bk.flat, s));
+  } else {
+    if (e0) HIPB_RET(hipEventRecord(e0, s));
+    if (e1) HIPB_RET(hipEventRecord(e1, s));
   }
   bk.unpacked = true;
   return GS_OK;
@@ -204,15 +240,20 @@ int launch_bucket(gs_bucketer* b, int bi) {
     // cross-stream hop to start it (its "queue") and none back at finalize.
     // The producer first joins the comm stream's earlier buckets, so the
     // communicator's collectives stay in issue order on the GPU.
-    const bool on_producer = b->tail_on_producer && bi == static_cast<int>(b->buckets.size()) - 1;
+    const bool last = bi == static_cast<int>(b->buckets.size()) - 1;
+    const bool on_producer = last;
     hipStream_t ps = static_cast<hipStream_t>(b->producer);
     hipStream_t cs = on_producer ? ps : comm_stream(b->comm);
     // timing events stay out of a hipGraph capture (the timeline then reports -1)
     const bool capturing = stream_capturing(cs);
-    const bool last = bi == static_cast<int>(b->buckets.size()) - 1;
     bk.ready_timed = !capturing && (b->timeline >= 2 || (b->timeline == 1 && last));
-    hipEvent_t ready = bk.ready_timed ? bk.ev_ready : bk.ev_sync;
-    HIPB_RET(hipEventRecord(ready, ps));
+    // the ready mark: a comm-stream chain waits on it; a producer-side tail needs
+    // it only as the start of the timed tail (no packet otherwise)
+    if (bk.ready_timed) {
+      HIPB_RET(hipEventRecord(bk.ev_ready, ps));
+    } else if (!on_producer) {
+      HIPB_RET(hipEventRecord(bk.ev_sync, ps));
+    }
     if (on_producer) {
       if (bi > 0) {
         HIPB_RET(hipEventRecord(b->ev_comm, comm_stream(b->comm)));
@@ -220,18 +261,44 @@ int launch_bucket(gs_bucketer* b, int bi) {
       }
       b->tail_ran_on_producer = true;
     } else {
-      HIPB_RET(hipStreamWaitEvent(cs, ready, 0));
+      HIPB_RET(hipStreamWaitEvent(cs, bk.ready_timed ? bk.ev_ready : bk.ev_sync, 0));
     }
     const bool timed = !capturing && b->timeline >= 2;
-    if (timed) HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
-    GS_TRY_RET(pack_one(b, bk, cs));
-    if (timed) HIPB_RET(hipEventRecord(bk.ev_t0, cs));
-    GS_TRY_RET(launch_collective(b, bk, cs));
-    if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
     bk.timed = timed;
+    // the producer-side tail at timeline >= 1: its last kernel marks "every chain
+    // done" itself (finalize then records nothing) — level 2: ev_u1, level 1: ev_done
+    const bool chain_end = !capturing && on_producer && b->timeline >= 1 && (b->do_unpack() || b->found_inf);
+    hipEvent_t end_ev = chain_end ? (timed ? bk.ev_u1 : b->ev_done) : (timed ? bk.ev_u1 : nullptr);
+    b->done_on_chain = chain_end;
+    if (chain_end) b->done_ev = end_ev;
+    // pack: ext start / stop = pk0 / t0 (the pack or the grad-view scaling, whichever runs)
+    if (timed) {
+      arm(bk.plan, bk.ev_pk0, bk.ev_t0);
+      arm(bk.flat, bk.ev_pk0, bk.ev_t0);
+    }
+    GS_TRY_RET(pack_raw(b, bk, cs));
+    if (timed) {
+      // the launch consumed the events of the plan it ran on; the other plan's are dropped,
+      // and any left unconsumed on both (no kernel ran) are recorded here
+      const bool taken = bk.plan->once_start == nullptr || bk.flat->once_start == nullptr;
+      if (taken) {
+        arm(bk.plan, nullptr, nullptr);
+        arm(bk.flat, nullptr, nullptr);
+      } else {
+        arm(bk.flat, nullptr, nullptr);
+        GS_TRY_RET(settle(bk.plan, cs));
+      }
+    }
+    GS_TRY_RET(debug_sum(b, bk, 0, cs));
+    GS_TRY_RET(launch_collective(b, bk, cs));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
-    if (b->do_unpack() || b->found_inf) GS_TRY_RET(unpack_one(b, bk, cs, 0));
-    if (timed) HIPB_RET(hipEventRecord(bk.ev_u1, cs));
+    // unpack: ext start / stop = t1 / (u1 or the done mark); the collective lies between t0 and t1
+    if (b->do_unpack() || b->found_inf) {
+      GS_TRY_RET(unpack_one(b, bk, cs, 0, timed ? bk.ev_t1 : nullptr, end_ev));
+    } else if (timed) {
+      HIPB_RET(hipEventRecord(bk.ev_t1, cs));
+      HIPB_RET(hipEventRecord(bk.ev_u1, cs));
+    }
     bk.stream = cs;
   } else {
     GS_TRY_RET(pack_one(b, bk, b->producer));
@@ -294,10 +361,6 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
   // div_factor is the world size (DDP / ZeRO divide by it); without a
   // communicator (host / external collectives) it is the only source of it
   const int world = comm ? gs_comm_world(comm) : std::max(1, static_cast<int>(div_factor + 0.5f));
-  static const int bucket_grid = [] {
-    const char* e = std::getenv("GSYNC_BUCKET_GRID");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
   for (int bi = 0; bi < n_buckets; ++bi) {
     Bucket& bk = b->buckets[bi];
     std::vector<int64_t> nm;
@@ -320,12 +383,6 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
     }
     rc = gs_plan_create(device_kind, device, 1, &bk.numel, 0, &bk.flat);
     if (rc != GS_OK) return bail(rc);
-    if (bucket_grid > 0) {  // GSYNC_BUCKET_GRID: workgroups of the in-step bucket kernels (A/B runs)
-      for (gs_plan* q : {bk.plan, bk.flat}) {
-        q->grid_cap = std::min(q->grid_cap, bucket_grid);
-        q->grid = std::min(q->grid, bucket_grid);
-      }
-    }
     bk.pending = static_cast<int>(bk.params.size());
     bk.gdt = grad_dtype;
     bk.bdt = bucket_dtype;
@@ -340,10 +397,6 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
   for (int p = 0; p < n_params; ++p)
     if (b->loc_bucket[p] < 0)
       return bail(fail(GS_EINVAL, "gs_bucketer_create: parameter " + std::to_string(p) + " is in no bucket"));
-  {
-    const char* e = std::getenv("GSYNC_TAIL_ON_PRODUCER");
-    b->tail_on_producer = !(e && std::atoi(e) == 0);
-  }
   if (device_kind == GS_DEV_HIP &&
       (hipEventCreateWithFlags(&b->ev_comm, hipEventDisableTiming) != hipSuccess ||
        hipEventCreate(&b->ev_done) != hipSuccess ||
@@ -490,8 +543,14 @@ int gs_bucketer_finalize(gs_bucketer* b, void* stream) {
     b->done_timed = b->timeline >= 1 && !stream_capturing(ds);
     hipEvent_t done = b->done_timed ? b->ev_done : b->ev_done_sync;
     // the last bucket ran on the producer after joining the comm stream:
-    // everything is already ordered before this point; otherwise join the comm stream
-    if (!on_ps || b->done_timed) HIPB_RET(hipEventRecord(done, ds));
+    // everything is already ordered before this point; otherwise join the comm stream.
+    // A producer-side tail whose last kernel carried the done mark records nothing.
+    const bool marked = on_ps && b->done_on_chain;
+    if (!on_ps || (b->done_timed && !marked)) {
+      HIPB_RET(hipEventRecord(done, ds));
+      b->done_ev = done;
+    }
+    b->done_on_chain = false;
     if (!on_ps) HIPB_RET(hipStreamWaitEvent(ps, done, 0));
   } else {
     // external collectives (comm hook / process group) are done by now
@@ -551,9 +610,9 @@ int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out) {
     HIPB_RET(hipEventElapsedTime(&out[2], bk.ev_t0, bk.ev_t1));
     HIPB_RET(hipEventElapsedTime(&out[3], bk.ev_t1, bk.ev_u1));
   }
-  if (bk.ready_timed && b->done_timed) {
-    HIPB_RET(hipEventSynchronize(b->ev_done));
-    HIPB_RET(hipEventElapsedTime(&out[4], bk.ev_ready, b->ev_done));
+  if (bk.ready_timed && b->done_timed && b->done_ev) {
+    HIPB_RET(hipEventSynchronize(b->done_ev));
+    HIPB_RET(hipEventElapsedTime(&out[4], bk.ev_ready, b->done_ev));
   }
   return GS_OK;
 }

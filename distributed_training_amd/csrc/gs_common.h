@@ -65,22 +65,16 @@ inline bool is_float_dtype(int dt) { return dt == GS_F32 || dt == GS_BF16 || dt 
 // <= kMaxSegPerTask segments; one workgroup processes one task at a time
 // (small tensors share a task; their descriptors are staged in LDS).
 constexpr int kUnit = 4;
-#ifndef GS_SEG_UNITS
-#define GS_SEG_UNITS 4096
-#endif
-constexpr int kSegUnits = GS_SEG_UNITS;   // max task: 16Ki elements = 64 KiB fp32 per stream
+constexpr int kSegUnits = 4096;   // max task: 16Ki elements = 64 KiB fp32 per stream
 constexpr int kMinTaskUnits = 256;        // one unit per lane of a 256-thread workgroup
-#ifndef GS_TARGET_TASKS
-#define GS_TARGET_TASKS 1920
-#endif
-constexpr int kTargetTasks = GS_TARGET_TASKS;  // < 2048 resident: ragged tensor ends add tasks
+constexpr int kTargetTasks = 1920;  // < 2048 resident: ragged tensor ends add tasks
 constexpr int kMaxSegPerTask = 64;
 constexpr int kBlock = 256;         // 4 waves of 64
 // default grid: one workgroup per task up to kGridLimit (the dispatcher refills
 // CUs faster than a resident grid loops: profiles/r1r_copy_micro.jsonl,
-// r1r_grid_sweep.jsonl); GS_MAX_GRID=2048 restores the one-resident-wave cap
+// r1r_grid_sweep.jsonl)
 constexpr int kMaxGrid = 65536;
-constexpr int kGridLimit = 65536;   // hard cap (partials buffer); GS_MAX_GRID env for tuning
+constexpr int kGridLimit = 65536;   // hard cap (partials buffer)
 // fused reductions: at most kRedMaxGroups group sums (one per lane of the
 // folding wave), each counter / group sum on its own 128-B line
 constexpr int kRedMaxGroups = GS_RED_GROUPS;
@@ -130,7 +124,7 @@ struct PlanArgs {
   int32_t red_acc;            // accumulate into red_out
   int32_t red_fuse;           // R > 0: combine in-kernel (two-level ticket, R groups), no combine launch
   int32_t red_groups_only;    // stop after the group level: the R group sums stay for a clipped update
-  int32_t per_wg;             // chunk engine: groups per workgroup (0 = grid-stride)
+  int32_t red_raw;            // one partial per workgroup straight to red_out (no counters, no combine)
   int32_t n;
   int32_t n_tasks;
   int32_t n_chunks;
@@ -203,8 +197,12 @@ struct gs_plan {
   int ring = 0;
   void* ring_events[4] = {nullptr, nullptr, nullptr, nullptr};
   void* last_stream = nullptr;
-  void* last_event = nullptr;
+  void* last_event = nullptr;   // recorded on last_stream only when a launch moves to another stream
   bool last_captured = false;   // the last launch was recorded into a stream capture
+  // one-shot HIP events for the next launch (the bucketer's timeline): written by
+  // that kernel's own dispatch (hipExtLaunchKernel start / stop), not as packets
+  void* once_start = nullptr;
+  void* once_stop = nullptr;
   unsigned long long table_capture_id = 0;  // capture that last recorded a table write
   bool in_graph = false;        // a graph holds a table write: re-upload before eager launches
   const float* hyper = nullptr; // device hyper-parameter source of sgd/adam (gs_plan_set_hyper_source)

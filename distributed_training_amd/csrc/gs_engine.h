@@ -4,15 +4,13 @@
 // Device code: include from .hip sources only.
 //
 // All of them are HBM-streaming kernels (no MFMA: nothing here is a
-// contraction).  One work decomposition serves every op: a plan cuts each
-// tensor into 4-element units, units into segments (<= 16 Ki elements) and
-// segments into tasks (<= 16 Ki elements, <= 64 segments).  A 256-thread
-// workgroup (4 wave64) takes one task at a time; the task's segment
-// descriptors are staged in LDS so that a workgroup gathers many small
-// tensors (BN weights/biases, 1x1-conv biases ...) in one pass with every
-// lane busy, while a large tensor gets one segment per task.  Every lane
-// moves 4 elements per access (16 B for fp32, 8 B for bf16/fp16) with ILP
-// accesses in flight before the first use.
+// contraction).  One engine serves every op (chunk_kernel): a plan lays its
+// tensors end to end in a virtual element space cut into 1 Ki-element chunks;
+// a 256-thread workgroup (4 wave64) takes G consecutive chunks per iteration
+// and grid-strides.  A group inside one tensor streams from a wave-uniform
+// (SGPR) base with G 16-B (fp32) / 8-B (16-bit) accesses per lane in flight;
+// chunks where tensors meet (tensor tails, runs of BN weights / biases) stage
+// the span's descriptors in LDS and resolve each lane's tensor there.
 //
 // Arithmetic is written with explicit fmaf and compiled with
 // -ffp-contract=off so that the host restatement (oracle/gs_oracle.c) and
@@ -106,29 +104,15 @@ __device__ __forceinline__ GLOBAL_AS T* gptr_w(void* p) {
   return (GLOBAL_AS T*)(p);
 }
 
-// Build-time tuning knobs (defaults are the measured best)
-#ifndef GS_NT_LOAD
-#define GS_NT_LOAD 0
-#endif
-// Non-temporal loads in the fused updates (profiles/r4/r4c_nt_instep.jsonl,
-// r4e_nt_state.jsonl: bench.py in the training step + the beyond-Infinity-Cache
-// rows, library variants interleaved, two rounds):
-// * the read-once gradient stream: unless a Σg² pass of the plan read it just before
-//   (in-step ResNet-50 SGD 0.786 -> 0.805-0.816 of 8 TB/s; back-to-back ResNet-152 x 2
-//   SGD 0.709 -> 0.729; but the clip path's update, right behind the Σg² kernel that
-//   brought the grads into the caches, 0.770 -> 0.740 with NT grad loads);
-// * the parameter / optimizer-state streams (p, momentum, exp_avg, exp_avg_sq): never
-//   by default.  Back to back beyond the cache NT loads there lift SGD to 0.76, but
-//   in the training step they cost every configuration measured — ResNet-50 SGD
-//   0.79 -> 0.70, ResNet-50 Adam 0.82 -> 0.73, ResNet-152 SGD (481 MB of state, far
-//   beyond the cache) 0.83 -> 0.74.  GS_NT_STATE (env) = 1 forces them, 2 = only
-//   when p + the fp32 states exceed the 256 MiB cache (the A/B rule measured above).
-#ifndef GS_NT_LOAD_GRAD
-#define GS_NT_LOAD_GRAD 1
-#endif
-#ifndef GS_NT_STATE_DEFAULT
-#define GS_NT_STATE_DEFAULT 0
-#endif
+// Load / store policy (measured)
+// * The update's read-once gradient stream takes non-temporal loads unless a Σg²
+//   pass of the plan read it just before and it fits the Infinity Cache (in-step
+//   ResNet-50 SGD 0.786 -> 0.805-0.816 of 8 TB/s; beyond the cache 0.709 -> 0.729;
+//   the clip path's update right behind its Σg² 0.770 -> 0.740 with NT loads:
+//   profiles/r4/r4c_nt_instep.jsonl).  The parameter / optimizer-state streams keep
+//   cached loads: NT there cost every in-step configuration measured (ResNet-50 SGD
+//   0.79 -> 0.70, Adam 0.82 -> 0.73, ResNet-152 SGD 0.83 -> 0.74, r4e_nt_state.jsonl).
+// * Every store is non-temporal (written once, read by another kernel much later).
 constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 
 // A stream read once takes non-temporal loads when it is larger than the
@@ -144,52 +128,25 @@ constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 // after RCCL wrote the shard, they cost 10 % (12.9 -> 14.2 us, r4v), and on the
 // bench's resident grads 2-5 % (r4u).  The DDP clip chain has a better answer
 // than NT loads, the Σg² folded into the unpack (fuse_grad_norm_into).
-// GS_NT_READ_ONCE / GS_NT_SQNORM: 0 never, 1 always, 2 the size rule (A/B).
-#ifndef GS_NT_READ_ONCE_DEFAULT
-#define GS_NT_READ_ONCE_DEFAULT 2
-#endif
-#ifndef GS_NT_SQNORM_DEFAULT
-#define GS_NT_SQNORM_DEFAULT 2
-#endif
+// GS_NT_READ_ONCE / GS_NT_SQNORM (environment): 0 never, 1 always, 2 the size rule
+// (default) — tests/test_clip_fold.py checks that no policy changes a bit.
 inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
   static const int policy = [] {
     const char* e = std::getenv("GS_NT_READ_ONCE");
-    return e ? std::atoi(e) : GS_NT_READ_ONCE_DEFAULT;
+    return e ? std::atoi(e) : 2;
   }();
   static const int policy_sq = [] {
     const char* e = std::getenv("GS_NT_SQNORM");
-    return e ? std::atoi(e) : GS_NT_SQNORM_DEFAULT;
+    return e ? std::atoi(e) : 2;
   }();
   const int pol = sqnorm ? policy_sq : policy;
   return pol == 2 ? stream_bytes > kInfinityCacheBytes : pol != 0;
 }
 inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
-#ifndef GS_NT_STORE
-#define GS_NT_STORE 1
-#endif
-#ifndef GS_PACK_ILP
-#define GS_PACK_ILP 4
-#endif
-#ifndef GS_OPT_ILP
-#define GS_OPT_ILP 2
-#endif
-// read-only reductions (Σg²) keep more loads in flight per lane
-#ifndef GS_RED_ILP
-#define GS_RED_ILP 4
-#endif
-// elements per lane-step (4 or 8): 8 gives 16-B accesses to 16-bit streams
-#ifndef GS_PACK_N
-#define GS_PACK_N 4
-#endif
-#ifndef GS_OPT_N
-#define GS_OPT_N 4
-#endif
-// chunks per workgroup iteration (chunk-map engine), per op; measured in
-// profiles/r2*_kernels_*.jsonl (scripts/r2_engine_ab.sh)
-// in-kernel combine of capped chunk-engine reductions (two-level ticket over
-// GS_RED_FUSE groups) instead of the combine_partials launch (0); the
-// environment variable of the same name overrides.
-// A single-counter ticket measured slower than the launch (r2c).
+// in-kernel combine of chunk-engine reductions (two-level ticket over R groups)
+// instead of the combine_partials launch (0); GS_RED_FUSE=<R> in the environment
+// overrides (tests/test_clip_fold.py).  A single-counter ticket measured slower
+// than the launch (r2c).
 #ifndef GS_RED_FUSE
 #define GS_RED_FUSE 64
 #endif
@@ -198,14 +155,16 @@ inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
 #endif
 constexpr int kRedSyncWords = (2 * kRedMaxGroups + 1) * kRedSyncStride;
 constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too many arrivals
+// chunks per workgroup iteration (chunk-map engine), per op: profiles/r2*_kernels_*.jsonl,
+// r3d (fp32 -> 16-bit pack: 8 > 2 = 4 > 1), r4k (ZeRO's bf16 -> bf16 pack: 4 > 2 > 8 > 1)
 #ifndef GS_G_PACK
 #define GS_G_PACK 1     // fp32 bucket
 #endif
 #ifndef GS_G_PACK16
-#define GS_G_PACK16 8   // fp32 grads -> 16-bit bucket (r3d sweep: 8 > 2 = 4 > 1)
+#define GS_G_PACK16 8   // fp32 grads -> 16-bit bucket
 #endif
 #ifndef GS_G_PACK16_16
-#define GS_G_PACK16_16 4  // 16-bit grads -> 16-bit bucket, ZeRO's bf16 pack (r4k sweep: 4 > 2 > 8 > 1)
+#define GS_G_PACK16_16 4  // 16-bit grads -> 16-bit bucket, ZeRO's bf16 pack
 #endif
 #ifndef GS_G_UNPACK
 #define GS_G_UNPACK 2
@@ -221,33 +180,22 @@ constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too 
 #endif
 // 256-thread workgroups are admitted 8 per CU only while the kernel uses <= 80
 // SGPRs (MI355X_MICROARCH.md, residency); cap the allocation there
-#ifndef GS_NUM_SGPR
-#define GS_NUM_SGPR 80
-#endif
-#if GS_NUM_SGPR > 0
-#define GS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GS_NUM_SGPR)))
-#else
-#define GS_SGPR_ATTR
-#endif
+#define GS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(80)))
 
-template <bool NT = (GS_NT_LOAD != 0), class V>
+template <bool NT = false, class V>
 __device__ __forceinline__ V vload(const GLOBAL_AS V* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
 }
 template <class V>
 __device__ __forceinline__ void vstore(GLOBAL_AS V* p, V v) {
-#if GS_NT_STORE
   __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
 }
 
 // load N (4 or 8) consecutive elements [e, e+N) of a tensor with n elements;
 // e is a multiple of N.  fp32: N/4 16-B loads; 16-bit: one 8-B (N=4) or
 // 16-B (N=8) load.  `vec`: the tensor base is 16-B aligned.
-template <int DT, int N, bool NT = (GS_NT_LOAD != 0)>
+template <int DT, int N, bool NT = false>
 __device__ __forceinline__ void loadN(const void* base, int64_t e, int64_t n, bool vec,
                                       float (&x)[N]) {
   static_assert(N == 4 || N == 8, "4 or 8 elements per lane");
@@ -337,7 +285,7 @@ template <int DT>
 __device__ __forceinline__ const void* elem_at(const void* base, int64_t e0) {
   return static_cast<const char*>(base) + e0 * (DT == GS_F32 ? 4 : 2);
 }
-template <int DT, bool NT = (GS_NT_LOAD != 0)>
+template <int DT, bool NT = false>
 __device__ __forceinline__ void load4F(const void* base, uint32_t lo, float (&x)[4]) {
   if constexpr (DT == GS_F32) {
     const gf4 v = vload<NT>((const GLOBAL_AS gf4*)(gptr<float>(base) + lo));
@@ -365,7 +313,7 @@ __device__ __forceinline__ void store4F(void* base, uint32_t lo, const float (&x
 }
 // F = full-chunk fast path (above); otherwise element e0 + lo of a tensor of
 // n elements with the bounds / alignment checks of loadN / storeN
-template <int DT, int N, bool F, bool NT = (GS_NT_LOAD != 0)>
+template <int DT, int N, bool F, bool NT = false>
 __device__ __forceinline__ void ld(const void* base, int64_t e0, uint32_t lo, int64_t n, bool vec,
                                    float (&x)[N]) {
   if constexpr (F) {
@@ -461,79 +409,6 @@ struct TV {
 template <class Op>
 __device__ __forceinline__ void load_hyper(Op&) {}
 
-template <int ILP, class Op>
-__device__ __forceinline__ void run_units(const Op& op, const TV* s_tv, const int64_t* s_ubeg,
-                                          const int32_t* s_pref, int ns, int total, float& acc) {
-  // a lane-step covers U consecutive units (U = Op::kN / 4); segments hold an
-  // even number of units (the plan pads), so a step never straddles two
-  constexpr int U = Op::kN / kUnit;
-  if (ns == 1) {
-    // one (large) tensor segment: descriptor in registers, no per-unit search
-    const TV v = s_tv[0];
-    const int64_t ub = s_ubeg[0];
-    for (int base = 0; base < total; base += kBlock * ILP * U) {
-      typename Op::Frag f[ILP];
-#pragma unroll
-      for (int j = 0; j < ILP; ++j) {
-        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-        if (u < total) op.template load<false>(v, (ub + u) * kUnit, 0u, f[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < ILP; ++j) {
-        const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-        if (u < total) op.template apply<false>(v, (ub + u) * kUnit, 0u, f[j], acc);
-      }
-    }
-    return;
-  }
-  // many small tensors share the task: binary search in the LDS prefix
-  for (int base = 0; base < total; base += kBlock * ILP * U) {
-    typename Op::Frag f[ILP];
-    int kk[ILP];
-    int64_t ee[ILP];
-#pragma unroll
-    for (int j = 0; j < ILP; ++j) {
-      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-      kk[j] = -1;
-      if (u < total) {
-        int lo = 0, hi = ns - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (s_pref[mid] <= u) lo = mid; else hi = mid - 1;
-        }
-        kk[j] = lo;
-        ee[j] = (s_ubeg[lo] + (u - s_pref[lo])) * kUnit;
-        op.template load<false>(s_tv[lo], ee[j], 0u, f[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < ILP; ++j)
-      if (kk[j] >= 0) op.template apply<false>(s_tv[kk[j]], ee[j], 0u, f[j], acc);
-  }
-}
-
-// part `part` of `parts` of one tensor of `total` units: lane-step chunks of
-// C = kBlock * ILP * U units, chunk c taken by part c % parts
-template <int ILP, class Op>
-__device__ __forceinline__ void run_interleaved(const Op& op, const TV& v, int part, int parts, int total,
-                                                float& acc) {
-  constexpr int U = Op::kN / kUnit;
-  constexpr int C = kBlock * ILP * U;
-  for (int base = part * C; base < total; base += parts * C) {
-    typename Op::Frag f[ILP];
-#pragma unroll
-    for (int j = 0; j < ILP; ++j) {
-      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-      if (u < total) op.template load<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < ILP; ++j) {
-      const int u = base + (j * kBlock + static_cast<int>(threadIdx.x)) * U;
-      if (u < total) op.template apply<false>(v, static_cast<int64_t>(u) * kUnit, 0u, f[j], acc);
-    }
-  }
-}
-
 // The plan tables are read-only for the whole launch: reading them through
 // the constant address space lets the uniform descriptor loads of a
 // single-segment task go to the scalar unit (s_load), with no LDS round trip
@@ -566,47 +441,6 @@ __device__ __forceinline__ TV load_tv(const Op& op, const PlanArgs& P, int t) {
   v.off = SCALAR ? cload(P.off, t) : P.off[t];
   v.pad = 0;
   return v;
-}
-
-template <int ILP, class Op>
-__global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR mt_kernel(PlanArgs P, Op op) {
-  __shared__ TV s_tv[kMaxSegPerTask];
-  __shared__ int64_t s_ubeg[kMaxSegPerTask];
-  __shared__ int32_t s_pref[kMaxSegPerTask + 1];
-  float acc = 0.f;
-  load_hyper(op);             // uniform: graph-replayable lr / bias corrections, clip coefficient
-  if (!op.active()) return;  // uniform across the grid
-  for (int task = blockIdx.x; task < P.n_tasks; task += gridDim.x) {
-    const int sb = cload(P.task_begin, task);
-    const int ns = cload(P.task_begin, task + 1) - sb;
-    if (ns == 1) {
-      // one (large) tensor segment: wave-uniform descriptor in SGPRs
-      const CONST_AS Seg* q = ((const CONST_AS Seg*)(P.segs)) + sb;
-      const int t = q->tensor;
-      const int64_t ub = q->unit_begin;
-      const int units = q->units;
-      const int parts = q->pad;
-      const TV v = load_tv<true>(op, P, t);
-      if (parts > 0) run_interleaved<ILP>(op, v, static_cast<int>(ub), parts, units, acc);
-      else run_units<ILP>(op, &v, &ub, nullptr, 1, units, acc);
-      continue;
-    }
-    if (threadIdx.x < ns) {
-      const Seg sg = P.segs[sb + threadIdx.x];
-      const int t = sg.tensor;
-      s_tv[threadIdx.x] = load_tv<false>(op, P, t);
-      s_ubeg[threadIdx.x] = sg.unit_begin;
-      s_pref[threadIdx.x] = sg.task_off;
-      if (threadIdx.x == ns - 1) s_pref[ns] = sg.task_off + sg.units;
-    }
-    __syncthreads();
-    run_units<ILP>(op, s_tv, s_ubeg, s_pref, ns, s_pref[ns], acc);
-    __syncthreads();
-  }
-  if constexpr (Op::kRed != 0) {
-    const float r = block_reduce<Op::kRed == 2>(acc);
-    if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
-  }
 }
 
 // deterministic combine of the per-workgroup partials (fixed order): 1024
@@ -691,9 +525,6 @@ __device__ __forceinline__ void chunk_mixed(const Op& op, const PlanArgs& P, int
 // (runs of tiny or empty tensors) keep the global path.  The caller's branch
 // is uniform across the workgroup (the chunk's code), so the barriers are too.
 // Measured: profiles/r2mlds/ (tiny tensors pack -15 %, R50 neutral).
-#ifndef GS_MIXED_LDS
-#define GS_MIXED_LDS 1
-#endif
 constexpr int kMixedStage = 64;  // tensors per mixed chunk staged (5 KB of LDS)
 template <class Op>
 __device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
@@ -721,28 +552,6 @@ __device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P,
   op.template apply<false>(v, local, 0u, f, acc);
 }
 
-// Stream-major issue (GS_STREAM_MAJOR=1, ops that expose kStreams / load_s<F, S>):
-// the G accesses of stream 0, then of stream 1, ... instead of every stream of
-// access 0, then of access 1 (scripts/micro/stream_mix.hip: +0.5-1.4 % on a plain
-// 3R2W stream at G = 4, profiles/r4/r4z_stream_mix.jsonl)
-#ifndef GS_STREAM_MAJOR
-#define GS_STREAM_MAJOR 0
-#endif
-template <class Op, class = void>
-struct op_streams { static constexpr int value = 0; };
-template <class Op>
-struct op_streams<Op, std::void_t<decltype(Op::kStreams)>> { static constexpr int value = Op::kStreams; };
-
-template <int S, int G, class Op>
-__device__ __forceinline__ void load_streams(const Op& op, const TV& v, int64_t e0, uint32_t tid,
-                                             typename Op::Frag (&f)[G]) {
-  if constexpr (S < op_streams<Op>::value) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) op.template load_s<true, S>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
-    load_streams<S + 1, G>(op, v, e0, tid, f);
-  }
-}
-
 template <int G, class Op>
 __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int t, int64_t c0, float& acc) {
   // G chunks c0 .. c0+G-1, all inside tensor t
@@ -751,12 +560,8 @@ __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int 
   const uint32_t tid = threadIdx.x;
   typename Op::Frag f[G];
   if (op.fast_ok(v)) {
-    if constexpr (GS_STREAM_MAJOR != 0 && op_streams<Op>::value > 0) {
-      load_streams<0, G>(op, v, e0, tid, f);
-    } else {
 #pragma unroll
-      for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
-    }
+    for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template apply<true>(v, e0, j * kChunkElems + tid * kUnit, f[j], acc);
   } else {
@@ -780,11 +585,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   __shared__ TV s_tv[kMixedStage];                            // ... and descriptors
   const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
   const int* cw = &P.chunks[0].t0;  // [t0, code] pairs
-  // groups per workgroup: grid-stride (per_wg == 0) or a contiguous range
-  const int64_t g_begin = P.per_wg ? blockIdx.x * static_cast<int64_t>(P.per_wg) : blockIdx.x;
-  const int64_t g_end = P.per_wg ? std::min<int64_t>(n_groups, g_begin + P.per_wg) : n_groups;
-  const int64_t g_step = P.per_wg ? 1 : gridDim.x;
-  for (int64_t g = g_begin; g < g_end; g += g_step) {
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
     const int64_t c0 = g * G;
     const int t = cload(cw, 2 * c0);
     const int code = cload(cw, 2 * c0 + 1);
@@ -802,7 +603,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
       const int tj = j == 0 ? t : cload(cw, 2 * c);
       const int cj = j == 0 ? code : cload(cw, 2 * c + 1);
       if (cj == 0) chunk_full<1>(op, P, tj, c, acc);
-      else if (GS_MIXED_LDS && cj > 0 && cj <= kMixedStage) chunk_mixed_lds(op, P, tj, cj, c, acc, s_lo, s_hi, s_tv);
+      else if (cj > 0 && cj <= kMixedStage) chunk_mixed_lds(op, P, tj, cj, c, acc, s_lo, s_hi, s_tv);
       else if (cj > 0) chunk_mixed(op, P, tj, cj, c, acc);
     }
   }
@@ -810,7 +611,9 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
     constexpr bool MAX = Op::kRed == 2;
     const float r = block_reduce<MAX>(acc);
     if (!P.red_fuse) {
-      if (threadIdx.x == 0) op.partials[blockIdx.x] = r;
+      // raw (gs_sqnorm_partial_out on a small plan): the partial goes straight to the
+      // caller's buffer, stream-ordered for its consumer; else to the combine's input
+      if (threadIdx.x == 0) (P.red_raw ? P.red_out : op.partials)[blockIdx.x] = r;
       return;
     }
     // In-kernel combine, two-level ticket.  Workgroup b belongs to group
@@ -887,26 +690,10 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   }
 }
 
-// Which ops stream through the chunk-map engine (bit 1 << GS_OP_*); the rest
-// use the task engine.  GS_ENGINE=<mask> overrides (A/B runs).
-#ifndef GS_CHUNK_OPS
-#define GS_CHUNK_OPS 254
-#endif
-bool use_chunk_engine(int kind) {
-  static const int mask = [] {
-    const char* e = std::getenv("GS_ENGINE");
-    return e ? std::atoi(e) : GS_CHUNK_OPS;
-  }();
-  return (mask >> kind) & 1;
-}
 // reductions: at most Op::kRedGrid workgroups (= partials for the combine:
 // 8 Ki for the read-only Σg² / inf checks, uncapped for the unpack that
-// carries a fused Σg²; profiles/r2e_red.jsonl), each grid-striding or taking a
-// contiguous range of groups (GS_RED_CONTIG=1); GS_RED_GRID / GS_RED_CONTIG
-// in the environment override (sweeps)
-#ifndef GS_RED_CONTIG
-#define GS_RED_CONTIG 0
-#endif
+// carries a fused Σg²; profiles/r2e_red.jsonl); GS_RED_GRID in the environment
+// overrides (tests/test_clip_fold.py: the folded clip stays bit-identical)
 int red_grid_cap(int op_default) {
   static const int v = [] {
     const char* e = std::getenv("GS_RED_GRID");
@@ -926,24 +713,6 @@ int red_fuse_groups() {
   }();
   return v;
 }
-// updates on a capped grid of contiguous group ranges (GS_UPD_CONTIG=<grid>,
-// 0 = off: one group per workgroup); VERDICT r3's candidate for the SGD beyond
-// the cache, A/B only
-int upd_contig_grid() {
-  static const int v = [] {
-    const char* e = std::getenv("GS_UPD_CONTIG");
-    return e ? std::max(0, std::min(std::atoi(e), kGridLimit)) : 0;
-  }();
-  return v;
-}
-bool red_contiguous() {
-  static const bool v = [] {
-    const char* e = std::getenv("GS_RED_CONTIG");
-    return e ? std::atoi(e) != 0 : GS_RED_CONTIG != 0;
-  }();
-  return v;
-}
-
 // ---------------------------------------------------------------- ops
 template <int DT>
 __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
@@ -1170,8 +939,8 @@ struct UnscaleOp {
 };
 
 // SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
-// NTG / NTS: non-temporal loads of the grad / of p and the momentum buffer (above)
-template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
+// NTG: non-temporal loads of the grad (the load policy above; p and the state stay cached)
+template <int N, int GD, int LD, bool NTG = true>
 struct SgdOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_SGD;
@@ -1196,17 +965,9 @@ struct SgdOp {
   }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
+    ld<GS_F32, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
     ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
-    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
-  }
-  // one stream of load() (stream-major issue, chunk_full)
-  static constexpr int kStreams = 3;
-  template <bool F, int S>
-  __device__ void load_s(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    if constexpr (S == 0) ld<GS_F32, N, F, NTS>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.p);
-    else if constexpr (S == 1) ld<GD, N, F, NTG>(v.ptr[1], e0, lo, v.numel, v.vec(1), f.g);
-    else if (h.mom != 0.f && !h.first) ld<GS_F32, N, F, NTS>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
+    if (h.mom != 0.f && !h.first) ld<GS_F32, N, F>(v.ptr[2], e0, lo, v.numel, v.vec(2), f.b);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1232,7 +993,7 @@ struct SgdOp {
 };
 
 // Adam/AdamW: slots 0 = p, 1 = g, 2 = exp_avg, 3 = exp_avg_sq, 4 = low-precision copy
-template <int N, int GD, int LD, bool NTG = true, bool NTS = false>
+template <int N, int GD, int LD, bool NTG = true>
 struct AdamOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_ADAM;
@@ -1257,19 +1018,10 @@ struct AdamOp {
   }
   template <bool F>
   __device__ void load(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
+    ld<GS_F32, N, F>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
     ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
-    ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
-    ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
-  }
-  // one stream of load() (stream-major issue, chunk_full)
-  static constexpr int kStreams = 4;
-  template <bool F, int S>
-  __device__ void load_s(const TV& tv, int64_t e0, uint32_t lo, Frag& f) const {
-    if constexpr (S == 0) ld<GS_F32, N, F, NTS>(tv.ptr[0], e0, lo, tv.numel, tv.vec(0), f.p);
-    else if constexpr (S == 1) ld<GD, N, F, NTG>(tv.ptr[1], e0, lo, tv.numel, tv.vec(1), f.g);
-    else if constexpr (S == 2) ld<GS_F32, N, F, NTS>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
-    else ld<GS_F32, N, F, NTS>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
+    ld<GS_F32, N, F>(tv.ptr[2], e0, lo, tv.numel, tv.vec(2), f.m);
+    ld<GS_F32, N, F>(tv.ptr[3], e0, lo, tv.numel, tv.vec(3), f.v);
   }
   template <bool F>
   __device__ void apply(const TV& tv, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1305,8 +1057,11 @@ struct AdamOp {
 __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float* gscale) {
   float sq;
   if (c.groups > 0) {
+    // lane l: partials l, l + 64, ... in order (<= GS_RED_PARTIALS), then the tree;
+    // for <= 64 group sums exactly the fused combine's last step
     const int l = static_cast<int>(threadIdx.x & 63);
-    const float x = l < c.groups ? c.sq[l * c.stride] : 0.f;
+    float x = 0.f;
+    for (int j = l; j < c.groups; j += 64) x = x + c.sq[j * c.stride];
     sq = wave_sum(0.f + x);
   } else {
     sq = c.sq[0];
@@ -1331,16 +1086,16 @@ __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
 }
-template <int N, int GD, int LD, bool NTG, bool NTS>
-__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTG, NTS>& op) {
+template <int N, int GD, int LD, bool NTG>
+__device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTG>& op) {
   if (op.hyper) {
     op.h.lr = op.hyper[0];
     if (op.h.first < 0) op.h.first = op.hyper[1] != 0.f;  // device first-step flag (AMP skips)
   }
   load_grad_multiplier(op);
 }
-template <int N, int GD, int LD, bool NTG, bool NTS>
-__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTG, NTS>& op) {
+template <int N, int GD, int LD, bool NTG>
+__device__ __forceinline__ void load_hyper(AdamOp<N, GD, LD, NTG>& op) {
   if (op.hyper) {
     op.h.step_size = op.hyper[0];
     op.h.bc2s = op.hyper[1];
@@ -1378,18 +1133,13 @@ struct DeviceGuard {
 // end: hipExtLaunchKernel's events, written by the dispatch itself, instead of two
 // event packets queued around it, whose own processing added ~3 µs to every timed
 // launch (a fifth of a 17 µs Σg² kernel, profiles/r4/r4i_timer_ext.jsonl).
-// GS_TIMER_EXT=0 brings the packet pair back (A/B).
-bool timer_ext() {
-  static const bool v = [] {
-    const char* e = std::getenv("GS_TIMER_EXT");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
 
 // groups_only (gs_sqnorm_partial): the fused reduction stops at its R group
-// sums, which stay in the plan for the next clipped update (p->red_groups)
-template <int ILP, class Op>
+// sums, which stay in the plan for the next clipped update (p->red_groups);
+// groups_only = 2 (raw, gs_sqnorm_partial_out on a small plan): a balanced grid of
+// <= GS_RED_PARTIALS workgroups, each writing its partial to red_out
+constexpr int kRawGroupsMax = 2048;  // chunk groups up to which the raw form serves
+template <class Op>
 int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0,
            int groups_only = 0) {
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1403,16 +1153,20 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   GsRange r_launch("gs_kernel_launch");
   op.partials = p->d_partials;
-  const int nslots = stream_capturing(s) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
+  const bool capturing = stream_capturing(s);
+  // one-shot events (the bucketer's timeline) take the launch; the timer ring skips it
+  const bool once = !capturing && (p->once_start != nullptr || p->once_stop != nullptr);
+  const int nslots = (capturing || once) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
-  const bool ext = nslots && timer_ext();
-  hipEvent_t ev0 = nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk]) : nullptr;
-  hipEvent_t ev1 = nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]) : nullptr;
-  if (nslots && !ext) HIP_RET(hipEventRecord(ev0, s));
-  const bool chunk = use_chunk_engine(Op::kKind) && !p->chunks.empty();
-  int grid = p->grid;
+  const bool ext = once || nslots;
+  hipEvent_t ev0 = once ? static_cast<hipEvent_t>(p->once_start)
+                        : nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk]) : nullptr;
+  hipEvent_t ev1 = once ? static_cast<hipEvent_t>(p->once_stop)
+                        : nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]) : nullptr;
+  p->once_start = p->once_stop = nullptr;
   bool fused = false;
-  if (chunk) {
+  int grid = 1;
+  {
     const int64_t groups = (static_cast<int64_t>(p->chunks.size()) + Op::kG - 1) / Op::kG;
     const bool red = Op::kRed != 0 && (red_out || groups_only);
     // a streaming op carrying a reduction (the unpack's Σg² / inf check) runs one group
@@ -1425,40 +1179,35 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     int cap = red ? std::min(p->grid_cap, red_grid_cap(op_cap)) : p->grid_cap;
     // groups_only is asked for only when the ordinary reduction would fuse too
     // (hip_sqnorm_partial), so both fold the same R group sums of the same grid
-    fused = red && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
+    const bool raw = red && groups_only == 2;
+    fused = red && !raw && (groups_only || (cap <= kRedFuseMaxGrid && red_fuse_groups() > 0));
     if (fused) cap = std::min(cap, red_grid_cap(Op::kRedFuseGrid));
     // any fused reduction overwrites the group sums a gs_sqnorm_partial left
     if (fused && !groups_only) p->red_valid = false;
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
-    PlanArgs a = p->args();
-    a.per_wg = (red && red_contiguous()) ? static_cast<int32_t>((groups + grid - 1) / grid) : 0;
-    if (!red && (Op::kKind == GS_OP_SGD || Op::kKind == GS_OP_ADAM) && upd_contig_grid() > 0) {
-      grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, upd_contig_grid())));
-      a.per_wg = static_cast<int32_t>((groups + grid - 1) / grid);
+    if (raw) {
+      // every workgroup the same number of groups (grid-stride over a balanced grid)
+      const int64_t per = (groups + GS_RED_PARTIALS - 1) / GS_RED_PARTIALS;
+      grid = static_cast<int>(std::max<int64_t>(1, (groups + per - 1) / per));
     }
+    PlanArgs a = p->args();
     a.red_out = Op::kRed != 0 ? red_out : nullptr;  // groups_only: the contiguous group sums (nullable)
     a.red_acc = accumulate;
     a.red_fuse = fused ? red_fuse_groups() : 0;
-    a.red_groups_only = groups_only;
-    if (groups_only) p->red_groups = std::min(grid, red_fuse_groups());
+    a.red_groups_only = groups_only ? 1 : 0;
+    a.red_raw = raw ? 1 : 0;
+    if (groups_only) p->red_groups = raw ? grid : std::min(grid, red_fuse_groups());
     a.ticket = reinterpret_cast<uint32_t*>(p->d_partials + kGridLimit);  // kRedSyncWords, zero between launches
-    const bool combine = Op::kRed != 0 && red_out && !fused;
+    const bool combine = Op::kRed != 0 && red_out && !fused && !raw;
     if (ext)
       hipExtLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, ev0, combine ? nullptr : ev1, 0, a,
                             op);
     else
       hipLaunchKernelGGL((chunk_kernel<Op>), dim3(grid), dim3(kBlock), 0, s, a, op);
-  } else {
-    const bool combine = Op::kRed != 0 && red_out;
-    if (ext)
-      hipExtLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, ev0, combine ? nullptr : ev1, 0,
-                            p->args(), op);
-    else
-      hipLaunchKernelGGL((mt_kernel<ILP, Op>), dim3(grid), dim3(kBlock), 0, s, p->args(), op);
   }
   HIP_RET(hipGetLastError());
   if constexpr (Op::kRed != 0) {
-    if (red_out && !fused) {
+    if (red_out && !fused && groups_only != 2) {
       if (ext)
         hipExtLaunchKernelGGL((combine_partials<Op::kRed == 2>), dim3(1), dim3(kCombineBlock), 0, s, nullptr, ev1, 0,
                               (const float*)p->d_partials, grid, red_out, accumulate);
@@ -1469,14 +1218,16 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     }
   }
   if (nslots) {
-    if (!ext) HIP_RET(hipEventRecord(ev1, s));
     p->timer_kind[tk] = Op::kKind;
     p->timer_next = (tk + 1) % nslots;
     p->timer_count = std::min(p->timer_count + 1, nslots);
   }
-  HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), s));
+  // No event packet after the launch: each one cost ~4.7 µs of stream time on every
+  // dependent chain (scripts/micro/event_chain.hip, profiles/r5/r5a_event_chain.jsonl).
+  // A launch on another stream orders itself after this one (hip_plan_flush); release
+  // synchronises before freeing.
   p->last_stream = stream;
-  p->last_captured = stream_capturing(s);
+  p->last_captured = capturing;
   return GS_OK;
 }
 

@@ -261,7 +261,13 @@ int host_unscale_check(gs_plan* p, int s_, int dt, const float* inv, float* foun
 // A lane a step does not write adds 0 (the DPP `old` operand is the identity).
 float host_wave_sum(const float* x, int n, int stride) {
   float v[64], t[64];
-  for (int l = 0; l < 64; ++l) v[l] = 0.f + (l < n ? x[static_cast<int64_t>(l) * stride] : 0.f);
+  // lane l first adds x[l], x[l + 64], ... in order (clip_multiplier's fold of up to
+  // GS_RED_PARTIALS partials), then the tree
+  for (int l = 0; l < 64; ++l) {
+    float a = 0.f;
+    for (int j = l; j < n; j += 64) a = a + x[static_cast<int64_t>(j) * stride];
+    v[l] = 0.f + a;
+  }
   auto step = [&](auto src, unsigned row_mask) {
     for (int l = 0; l < 64; ++l) t[l] = ((row_mask >> (l >> 4)) & 1u) ? v[src(l)] : 0.f;
     for (int l = 0; l < 64; ++l) v[l] = v[l] + t[l];

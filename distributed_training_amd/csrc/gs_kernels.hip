@@ -121,8 +121,12 @@ int hip_plan_timer_read(gs_plan* p, float* ms_out, int32_t* kind_out, int cap) {
 int hip_plan_release(gs_plan* p) {
   DeviceGuard g(p->device);
   (void)hip_plan_timer_enable(p, 0);
-  // make sure nothing in flight still reads the tables
-  if (p->last_event) (void)hipEventSynchronize(static_cast<hipEvent_t>(p->last_event));
+  // make sure nothing in flight still reads the tables: an event behind the plan's
+  // last launch (hipFree below synchronises the device as well, hip_runtime_api.h)
+  if (p->last_event && p->last_stream != nullptr && !p->last_captured && !stream_capturing(p->last_stream) &&
+      hipEventRecord(static_cast<hipEvent_t>(p->last_event), static_cast<hipStream_t>(p->last_stream)) ==
+          hipSuccess)
+    (void)hipEventSynchronize(static_cast<hipEvent_t>(p->last_event));
   for (int i = 0; i < 4; ++i) {
     if (p->ring_events[i]) {
       (void)hipEventSynchronize(static_cast<hipEvent_t>(p->ring_events[i]));
@@ -173,9 +177,16 @@ int hip_plan_flush(gs_plan* p, void* stream) {
   // both are eager or both belong to the capture (an event recorded inside a
   // capture cannot order eager work: graph replays are ordered by the caller,
   // as torch.cuda.graph requires)
+  // The event is recorded on the previous stream now, not after every launch (a packet
+  // per launch cost ~4.7 µs of stream time, scripts/micro/event_chain.hip): it
+  // follows everything enqueued there so far, the plan's last launch included.  A
+  // previous stream that entered or left a capture since cannot order this launch.
   if (p->last_stream != nullptr && p->last_stream != stream && capturing == p->last_captured &&
-      (!capturing || cid == p->table_capture_id))
+      (!capturing || cid == p->table_capture_id) &&
+      stream_capturing(p->last_stream) == p->last_captured) {
+    HIP_RET(hipEventRecord(static_cast<hipEvent_t>(p->last_event), static_cast<hipStream_t>(p->last_stream)));
     HIP_RET(hipStreamWaitEvent(s, static_cast<hipEvent_t>(p->last_event), 0));
+  }
   const size_t ptr_bytes = sizeof(void*) * GS_PLAN_SLOTS * p->n;
   const size_t tb = table_bytes(p);
   if (capturing) {
@@ -214,9 +225,9 @@ int hip_plan_flush(gs_plan* p, void* stream) {
 // ------------------------------------------------------------- dispatchers
 template <int SD, int FD, int MODE, bool NT>
 static int pack_mode(gs_plan* p, int src_slot, void* flat, float s, void* stream) {
-  PackOp<GS_PACK_N, SD, FD, MODE, NT> op;
+  PackOp<kUnit, SD, FD, MODE, NT> op;
   op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s;
-  return launch<GS_PACK_ILP>(p, op, stream);
+  return launch(p, op, stream);
 }
 
 template <bool NT>
@@ -247,9 +258,9 @@ template <int RED, bool NT>
 static int unpack_nt(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* red, int acc,
                      void* stream) {
   GS_DISPATCH_FLOAT(flat_dt, FD, GS_DISPATCH_FLOAT(dst_dt, DD, {
-    UnpackOp<GS_PACK_N, FD, DD, RED, NT> op;
+    UnpackOp<kUnit, FD, DD, RED, NT> op;
     op.want_red = red != nullptr; op.flat = flat; op.flat_vec = flat_aligned(flat); op.slot = dst_slot;
-    return launch<GS_PACK_ILP>(p, op, stream, red, acc);
+    return launch(p, op, stream, red, acc);
   }));
   return GS_OK;
 }
@@ -275,9 +286,9 @@ int hip_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, in
 int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    ScaleOp<GS_PACK_N, DT> op;
+    ScaleOp<kUnit, DT> op;
     op.slot = slot; op.s = s; op.mode = mode;
-    return launch<GS_PACK_ILP>(p, op, stream);
+    return launch(p, op, stream);
   });
   return GS_OK;
 }
@@ -285,28 +296,19 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
 template <bool NT>
 static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
-    SqnormOp<GS_PACK_N, DT, NT> op;
+    SqnormOp<kUnit, DT, NT> op;
     op.slot = slot;
-    return launch<GS_RED_ILP>(p, op, stream, sq, acc, groups_only);
+    return launch(p, op, stream, sq, acc, groups_only);
   });
   return GS_OK;
 }
-// A non-temporal Σg² leaves the grads out of the caches: the update that follows
-// then loads them non-temporally too (grads_read cleared).  GS_NT_SQ_HOT=1 keeps
-// the update's cached grad loads after it (A/B).
-static bool nt_sq_keeps_hot() {
-  static const bool v = [] {
-    const char* e = std::getenv("GS_NT_SQ_HOT");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
-
-// the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once)
+// the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once);
+// a non-temporal Σg² leaves the grads out of the caches, so the update that
+// follows loads them non-temporally too (grads_read cleared)
 static int sqnorm_launch(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
   if (!nt_read_once(p->elems * dtype_bytes(dt), true))
     return sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
-  if (!nt_sq_keeps_hot()) p->grads_read = false;
+  p->grads_read = false;
   return sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream);
 }
 
@@ -332,8 +334,16 @@ float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit
 // also contiguous in caller memory, or the finished Σ in groups_out[0].
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream) {
   DeviceGuard g(p->device);
-  const int cap = std::min(p->grid_cap, red_grid_cap(SqnormOp<GS_PACK_N, GS_F32>::kRedGrid));
-  const bool groups = use_chunk_engine(GS_OP_SQNORM) && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
+  // caller memory on a small plan (a ZeRO shard at N = 8): one partial per workgroup of a
+  // balanced grid, no counters and no combine — the kernel ends with its last store
+  const int64_t chunk_groups = (static_cast<int64_t>(p->chunks.size()) + GS_G_RED - 1) / GS_G_RED;
+  if (groups_out && !p->chunks.empty() && p->n > 0 && !p->segs.empty() && chunk_groups <= kRawGroupsMax) {
+    GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 2, stream));
+    if (n_groups) *n_groups = p->red_groups;
+    return GS_OK;
+  }
+  const int cap = std::min(p->grid_cap, red_grid_cap(SqnormOp<kUnit, GS_F32>::kRedGrid));
+  const bool groups = !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
                       red_fuse_groups() > 0 && cap <= kRedFuseMaxGrid;
   if (groups) {
     GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 1, stream));
@@ -352,9 +362,9 @@ int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t*
 int hip_sum(gs_plan* p, int slot, int dt, float* out, int acc, void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    SumOp<GS_PACK_N, DT> op;
+    SumOp<kUnit, DT> op;
     op.slot = slot;
-    return launch<GS_RED_ILP>(p, op, stream, out, acc);
+    return launch(p, op, stream, out, acc);
   });
   return GS_OK;
 }
@@ -384,10 +394,10 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
                       void* stream) {
   DeviceGuard g(p->device);
   GS_DISPATCH_FLOAT(dt, DT, {
-    UnscaleOp<GS_PACK_N, DT> op;
+    UnscaleOp<kUnit, DT> op;
     op.slot = slot; op.inv = inv;
     // found_inf accumulates (max) into the caller's flag, as torch's kernel does
-    return launch<GS_PACK_ILP>(p, op, stream, found, 1);
+    return launch(p, op, stream, found, 1);
   });
   return GS_OK;
 }

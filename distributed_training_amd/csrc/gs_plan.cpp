@@ -55,7 +55,7 @@ gs::PlanArgs gs_plan::args() const {
   a.red_acc = 0;
   a.red_fuse = 0;
   a.red_groups_only = 0;
-  a.per_wg = 0;
+  a.red_raw = 0;
   a.ptrs = static_cast<void* const*>(d_table);
   a.align = reinterpret_cast<const uint32_t*>(static_cast<char*>(d_table) +
                                               sizeof(void*) * GS_PLAN_SLOTS * n);
@@ -106,21 +106,12 @@ static void build_chunk_map(gs_plan* p) {
 // (kSegUnits): the interleaved sweep (profiles/r1d_sweep_tasks_nt.jsonl)
 // puts 64 Ki-element tasks 20-25 % below 8-16 Ki-element ones on pack/unpack
 // of 120 M-element plans, while a second round of tasks costs little there.
-// GS_TASK_UNITS=<n> / GS_TARGET_TASKS=<n> in the environment override (tuning runs).
 // Optimizer-update plans ask for 512-unit tasks instead (gs_plan_create_ex,
 // multi_tensor.UPDATE_TASK_UNITS): five streams per element make the
 // per-task descriptor prologue cheap relative to the data, and a short task
 // per workgroup streams +2-8 % faster (profiles/r1r_grid_sweep.jsonl).
 int64_t plan_task_units(int64_t total_units) {
-  static const int64_t forced = [] {
-    const char* e = std::getenv("GS_TASK_UNITS");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
-  }();
-  static const int64_t target = [] {
-    const char* e = std::getenv("GS_TARGET_TASKS");
-    return e && std::atoll(e) > 0 ? std::atoll(e) : int64_t(kTargetTasks);
-  }();
-  if (forced > 0) return std::max<int64_t>(kUnit, std::min<int64_t>(forced, int64_t(1) << 20));
+  const int64_t target = kTargetTasks;
   int64_t u = (total_units + target - 1) / target;
   u = (u + kBlock - 1) / kBlock * kBlock;
   return std::max<int64_t>(kMinTaskUnits, std::min<int64_t>(kSegUnits, u));
@@ -179,17 +170,13 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
       task_units_req > 0 ? std::max<int64_t>(kUnit, task_units_req) : plan_task_units(total_units);
   task_units += task_units & 1;  // even (see the segment padding below)
   p->task_units = task_units;
-  static const bool interleave = [] {
-    const char* e = std::getenv("GS_INTERLEAVE");
-    return e ? std::atoi(e) != 0 : true;
-  }();
   for (int t = 0; t < n_tensors; ++t) {
     int64_t units = (numels[t] + kUnit - 1) / kUnit;
     if (units == 0) continue;
     // even unit counts: an 8-element lane-step (two units) never straddles
     // segments; the padding unit lies past the tensor's end and is masked
     units += units & 1;
-    if (interleave && units > task_units) {
+    if (units > task_units) {
       // a tensor larger than a task is shared by M single-segment tasks in
       // interleaved chunks (part i takes lane-step chunks i, i+M, i+2M, ...):
       // the M workgroups sweep the tensor front to back together instead of M
@@ -231,11 +218,7 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
   }
   if (!p->segs.empty()) p->task_begin.push_back(static_cast<int32_t>(p->segs.size()));
   const int n_tasks = static_cast<int>(p->task_begin.size()) - 1;
-  static const int grid_cap = [] {
-    const char* e = std::getenv("GS_MAX_GRID");
-    const long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<int>(std::min<long>(v, kGridLimit)) : kMaxGrid;
-  }();
+  const int grid_cap = kMaxGrid;
   p->grid = std::max(1, std::min(n_tasks, grid_cap));
   build_chunk_map(p);
   p->grid_cap = grid_cap;
@@ -410,7 +393,7 @@ int gs_plan_set_clip_groups(gs_plan* p, const float* groups_dev, int32_t n_group
     return GS_OK;
   }
   GS_CHECK_ARG(groups_dev != nullptr, "gs_plan_set_clip_groups: NULL group sums");
-  GS_CHECK_ARG(n_groups >= 1 && n_groups <= GS_RED_GROUPS, "gs_plan_set_clip_groups: n_groups out of 1..64");
+  GS_CHECK_ARG(n_groups >= 1 && n_groups <= GS_RED_PARTIALS, "gs_plan_set_clip_groups: n_groups out of 1..512");
   GS_CHECK_ARG(eps >= 0.f, "gs_plan_set_clip_groups: eps < 0");
   p->clip_on = true;
   p->clip_own = false;

@@ -394,6 +394,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._buffers_plan = None
         self._sqnorm_target: torch.Tensor | None = None
         self._sqnorm_valid = False  # the last synchronising backward's unpacks filled _sqnorm_target
+        self._sqnorm_versions = None  # _grad_versions() when they did
         self._found_inf_target: torch.Tensor | None = None
         self._found_inf_valid = False
 
@@ -519,6 +520,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             self._wait_post_backward_futures()
         self._found_inf_valid = self._found_inf_target is not None
         self._sqnorm_valid = self._sqnorm_fusable()
+        self._sqnorm_versions = self._grad_versions() if self._sqnorm_valid else None
         if self.gradient_as_bucket_view:
             b = self._bucketer
             for i, p in enumerate(self._params):
@@ -676,9 +678,17 @@ class DistributedDataParallel(nn.Module, Joinable):
     def _bcast_flat(self, flat, root: int = 0):
         if self._comm is not None:
             self._comm.broadcast(flat, root=root, stream=L.stream_ptr(self.device))
+            return
+        src = dist.get_global_rank(self.process_group, root) if self.process_group is not dist.group.WORLD else root
+        if flat.is_cuda and self._backend == "gloo":
+            # a device tensor over gloo (ranks sharing a GPU: the rehearsal path) is staged
+            # through host memory, as the bucket all-reduces are (_launch_external): no
+            # collective of gloo's CUDA path runs on the rehearsal
+            host = flat.cpu()
+            dist.broadcast(host, src=src, group=self.process_group)
+            flat.copy_(host)
         else:
-            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, root)
-                           if self.process_group is not dist.group.WORLD else root, group=self.process_group)
+            dist.broadcast(flat, src=src, group=self.process_group)
 
     @torch.no_grad()
     def _sync_module_states(self):
@@ -945,6 +955,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             self._overlap_step(range(len(b.buckets)))
         self._found_inf_valid = self._found_inf_target is not None
         self._sqnorm_valid = self._sqnorm_fusable()
+        self._sqnorm_versions = self._grad_versions() if self._sqnorm_valid else None
         if self.find_unused_parameters:
             if self.world_size > 1:
                 self._grads_of_locally_unused()
@@ -1175,6 +1186,14 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _sqnorm_fusable(self) -> bool:
         return self._sqnorm_target is not None and not self.gradient_as_bucket_view
+
+    def _grad_versions(self) -> int:
+        """Σ of the grads' autograd version counters when the unpacks formed Σg²:
+        any in-place change of a grad after that (torch ops bump the counter;
+        libgsync's own in-place grad kernels — GradScaler.unscale_, clip_grad_norm_
+        — bump it explicitly) makes the fused Σg² stale (a scaled Σg²
+        folded after ``scaler.unscale_``)."""
+        return sum(p.grad._version for p in self._params if p.grad is not None)
 
     def set_timeline(self, level: int):
         """Which HIP timing events the bucket chains record

@@ -1,8 +1,9 @@
 """Python handle on a libgsync multi-tensor plan (``gs_plan``).
 
 A plan is a static list of tensor sizes laid out in one flat buffer, with the
-work decomposition (segments / tasks) built once; only the per-tensor pointer
-tables change from call to call, and they are re-uploaded only when they do.
+chunk map the device kernels stream through built once; only the per-tensor
+pointer tables change from call to call, and they are re-uploaded only when
+they do.
 It plays the role of ATen's ``multi_tensor_apply`` launch machinery
 (T:include/ATen/native/cuda/MultiTensorApply.cuh:14-21) for every op on the
 gradient-sync path.
@@ -10,21 +11,17 @@ gradient-sync path.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Sequence
 
 import torch
 
 from . import _lib as L
 
-# Task size (units of 4 elements) for optimizer-update plans on the GPU: 2 Ki
-# elements per workgroup, one workgroup per task.  The update kernels move
-# 20-28 B per element over five streams, so the per-task descriptor prologue
-# is cheap next to the data and short tasks stream faster than the default
-# one-resident-wave tasking: fused SGD +8 % on ResNet-50, +2 % on ResNet-152,
-# Adam +1-3 % (profiles/r1r_grid_sweep.jsonl).  Pack / unpack keep the default
-# sizing (short tasks cost them 20-50 % there).
-UPDATE_TASK_UNITS = int(os.environ.get("GSYNC_UPDATE_TASK_UNITS", "512"))  # 0 = library default (A/B runs)
+# Task size (units of 4 elements) of an optimizer-update plan's segment table on
+# the GPU (gs_plan_create_ex task_units).  The device kernels stream through the
+# chunk map (gs_engine.h) whatever the task size; the segment table stays the
+# plan's public work decomposition (gs_plan_n_tasks / gs_plan_task_units).
+UPDATE_TASK_UNITS = 512
 
 
 def update_task_units(device) -> int:
@@ -125,6 +122,16 @@ class TensorListPlan:
         n = L.check(L.lib().gs_plan_timer_read(self.handle, out, kinds, int(cap)), "gs_plan_timer_read")
         return [float(out[i]) for i in range(n) if kind is None or kinds[i] == kind]
 
+    def timer_read_by_kind(self, cap: int = 4096) -> dict:
+        """{GS_OP_* kind: [durations (ms)]} of the launches recorded since the last read."""
+        out = (ctypes.c_float * max(1, cap))()
+        kinds = (ctypes.c_int32 * max(1, cap))()
+        n = L.check(L.lib().gs_plan_timer_read(self.handle, out, kinds, int(cap)), "gs_plan_timer_read")
+        by: dict = {}
+        for i in range(n):
+            by.setdefault(int(kinds[i]), []).append(float(out[i]))
+        return by
+
     # ------------------------------------------------------------------ ops
     def pack(self, src_slot, src_dtype, flat: torch.Tensor, scale=1.0, mode=L.GS_SCALE_NONE, stream=None):
         L.check(
@@ -160,13 +167,15 @@ class TensorListPlan:
                 "gs_sqnorm_partial")
 
     def sqnorm_partial_out(self, slot, dtype, groups: torch.Tensor, stream=None) -> int:
-        """:meth:`sqnorm_partial` whose group sums also land contiguously in
-        ``groups`` (fp32, >= 64 elements, where the plan runs; gs_sqnorm_partial_out);
-        returns how many are valid.  Sharded optimizers SUM-all-reduce
-        ``groups[:n]`` across ranks, then :meth:`set_clip_groups`."""
-        if groups.dtype != torch.float32 or groups.numel() < L.GS_RED_GROUPS or not groups.is_contiguous() or \
+        """:meth:`sqnorm_partial` whose partial sums land contiguously in
+        ``groups`` (fp32, >= GS_RED_PARTIALS elements, where the plan runs;
+        gs_sqnorm_partial_out: one per workgroup of a balanced grid on a small
+        plan, else the <= 64 group sums); returns how many are valid.  Sharded
+        optimizers SUM-all-reduce the whole buffer across ranks (the slots past
+        n stay zero), then :meth:`set_clip_groups`."""
+        if groups.dtype != torch.float32 or groups.numel() < L.GS_RED_PARTIALS or not groups.is_contiguous() or \
                 (groups.device.type == "cuda") != (self.kind == L.GS_DEV_HIP):
-            raise ValueError(f"group sums: contiguous fp32[>= {L.GS_RED_GROUPS}] where the plan runs")
+            raise ValueError(f"partial sums: contiguous fp32[>= {L.GS_RED_PARTIALS}] where the plan runs")
         n = ctypes.c_int32()
         L.check(L.lib().gs_sqnorm_partial_out(self.handle, slot, L.gs_dtype(dtype), groups.data_ptr(),
                                               ctypes.byref(n), self._stream(stream)), "gs_sqnorm_partial_out")
@@ -175,7 +184,8 @@ class TensorListPlan:
     def set_clip_groups(self, max_norm: float | None, eps: float, groups: torch.Tensor, n_groups: int,
                         sq_mul: float = 1.0, coef_mul: float = 1.0, out: torch.Tensor | None = None):
         """:meth:`set_clip` with ‖g‖² = the fold of ``groups[:n_groups]``
-        (gs_plan_set_clip_groups), the update's workgroups folding them."""
+        (<= GS_RED_PARTIALS; gs_plan_set_clip_groups), the update's workgroups
+        folding them in a fixed order."""
         for t in (groups, out):
             if t is not None and (t.dtype != torch.float32 or (t.device.type == "cuda") != (self.kind == L.GS_DEV_HIP)):
                 raise ValueError("clip tensors: fp32, where the plan runs")

@@ -36,6 +36,7 @@ import os
 from typing import Iterable
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib as L
 from .multi_tensor import TensorListPlan, clip_coef, is_dense, update_task_units
@@ -177,16 +178,25 @@ class _FusedBase(torch.optim.Optimizer):
         self._norm_ddp = (ddp, frozenset(id(p) for p in ddp._params))
 
     def _ddp_sqnorm(self, device):
-        """The DDP's fused Σg² when it covers this step's grads (consumed)."""
+        """The DDP's fused Σg² when it covers this step's grads, unchanged since
+        the unpacks formed it (consumed).  A grad changed in place after backward
+        (``GradScaler.unscale_``, ``clip_grad_norm_``, any torch in-place op: the
+        grads' version counters moved) leaves the optimizer's own Σg² pass to run."""
         if self._norm_ddp is None:
             return None
         ddp, ids = self._norm_ddp
         if not ddp._sqnorm_valid or ddp.device != device:
             return None
-        mine = frozenset(id(p) for g in self.param_groups for p in g["params"] if p.grad is not None)
-        if mine != ids:
-            return None
+        mine, ver = set(), 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                gr = p.grad
+                if gr is not None:
+                    mine.add(id(p))
+                    ver += gr._version
         ddp._sqnorm_valid = False
+        if mine != ids or ver != ddp._sqnorm_versions:
+            return None
         return self._clip_buf[device][3:4]
 
     def _clip_scale(self, device, all_plans):
@@ -198,8 +208,11 @@ class _FusedBase(torch.optim.Optimizer):
         (gs_plan_set_clip) — one plan: from the plan's Σg² partial sums
         (gs_sqnorm_partial), so Σg² -> update is two launches with no combine
         and no coefficient launch between them; several plans (grad dtypes):
-        Σg² accumulated into one scalar first.  Bit-identical to the separate
-        path (GSYNC_CLIP_FUSED=0: Σg² + combine, gs_clip_coef, mul_ launches)."""
+        Σg² accumulated into one scalar first.  Those two forms are
+        bit-identical to the separate path (GSYNC_CLIP_FUSED=0: Σg² + combine,
+        gs_clip_coef, mul_ launches).  The DDP-fed form (fuse_grad_norm_into,
+        ``last_clip_source == "ddp_unpack"``) sums the same squares in bucket
+        order: its coefficient equals the others only to fp32 rounding."""
         max_norm = self.defaults.get("max_grad_norm")
         if not max_norm:
             for plan, _ in all_plans:
@@ -590,4 +603,7 @@ def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm:
         # unscale kernel with the coefficient as the (device) multiplier
         found = torch.zeros(1, dtype=torch.float32, device=dev)
         plan.unscale_check(0, dt, coef, found)
+    # the kernel wrote the grads in place: tell autograd's version counters, as a
+    # torch in-place op would (a DDP's fused Σg² of these grads is stale now)
+    increment_version(grads)
     return norm.reshape(())

@@ -85,7 +85,8 @@ class ZeroDataParallel:
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.0,
                  process_group=None, reduce_bucket_size: int = int(5e7), gradient_clipping: float = 0.0,
                  loss_scaler: DynamicLossScaler | None = None, broadcast_params: bool = True,
-                 capturable: bool = False):
+                 capturable: bool = False, overlap_allgather: bool = False,
+                 allgather_bucket_size: int | None = None):
         if stage not in (1, 2):
             raise NotImplementedError(f"ZeRO stage {stage}: only 1 and 2 are on the gradient-sync path")
         if not dist.is_initialized():
@@ -128,11 +129,22 @@ class ZeroDataParallel:
                 for t in list(self.params) + list(module.buffers()):
                     self._bcast(t.data if t.is_floating_point() else t)
 
-        # buckets in gradient-ready (reverse module) order, <= reduce_bucket_size elements
+        # buckets in gradient-ready (reverse module) order, <= reduce_bucket_size elements.
+        # overlap_allgather (opt-in; DeepSpeed's ZeRO-2 gathers everything at the end of
+        # step, R:resnet/deepspeed/deepspeed_train.py:210-216, and stays the default):
+        # buckets of <= allgather_bucket_size elements whose parameter all-gathers run on
+        # the communicator's stream behind the update, first layers first, each awaited
+        # by the first forward of a module holding its parameters (wait_allgather())
+        self.overlap_allgather = bool(overlap_allgather)
+        if self.overlap_allgather and self.capturable:
+            raise NotImplementedError("overlap_allgather: eager steps only (not with capturable)")
+        cap = int(reduce_bucket_size)
+        if self.overlap_allgather:
+            cap = min(cap, int(allgather_bucket_size or 5_000_000))
         n = len(self.params)
         order = list(reversed(range(n)))
         esz = self.params[0].element_size()
-        self.buckets = compute_bucket_assignment_by_size(self.params, [int(reduce_bucket_size) * esz], order=order)
+        self.buckets = compute_bucket_assignment_by_size(self.params, [cap * esz], order=order)
         self._make_bucketer()
         self._build_flat_state()
         self._hooks = []
@@ -141,8 +153,8 @@ class ZeroDataParallel:
         self._pending = {}
         # [found_inf, Σg² (all-reduced), 1/scale, -, clip out: Σg²·s², coefficient, ‖g‖]
         self._scratch = torch.zeros(8, dtype=torch.float32, device=self.device)
-        # world > 1 folded clip: this rank's Σg² group sums, then their SUM over ranks
-        self._red_groups = torch.zeros(L.GS_RED_GROUPS, dtype=torch.float32, device=self.device)
+        # world > 1 folded clip: this rank's Σg² partial sums, then their SUM over ranks
+        self._red_groups = torch.zeros(L.GS_RED_PARTIALS, dtype=torch.float32, device=self.device)
         self._capture_local: dict | None = None  # parity.py: {param index: local grad copy}
         # the per-gradient hook in C++ (_gshook, release mode: the grad is freed once its
         # pack is enqueued) on the library-collective path; Python hooks otherwise
@@ -153,13 +165,37 @@ class ZeroDataParallel:
         if self._native is not None:
             self._native_bind()
         self._set_native(self._native_ok())
+        self._ag_pending: set = set()
+        self._ag_hooks = []
+        self._ag_time = None  # (start, end) timing events around the step's all-gathers (time_allgather)
+        if self.overlap_allgather:
+            self._ag_ev = [torch.cuda.Event() if self.is_cuda else None for _ in self.buckets]
+            index = {id(p): i for i, p in enumerate(self.params)}
+            for m in module.modules():
+                bs = sorted({self.loc[index[id(p)]][0] for p in m.parameters(recurse=False) if id(p) in index})
+                if bs:
+                    self._ag_hooks.append(m.register_forward_pre_hook(
+                        lambda mod, inp, bs=tuple(bs): self._wait_buckets(bs)))
 
     # ------------------------------------------------------------------ setup
+    # Without the library communicator the collectives go through the process
+    # group; device tensors over gloo (ranks sharing a GPU: the rehearsal path)
+    # are staged through host memory, as the bucket all-reduces are — no
+    # collective of gloo's CUDA path runs
+    def _host_staged(self, t) -> bool:
+        return self._comm is None and t.is_cuda and dist.get_backend(self.pg) == "gloo"
+
     def _bcast(self, t):
         if self._comm is not None:
             self._comm.broadcast(t, 0, stream=L.stream_ptr(self.device))
+        elif self._host_staged(t):
+            host = t.cpu()
+            dist.broadcast(host, src=dist.get_global_rank(self.pg, 0) if self.pg is not dist.group.WORLD else 0,
+                           group=self.pg)
+            t.copy_(host)
         else:
-            dist.broadcast(t, src=0, group=self.pg)
+            dist.broadcast(t, src=dist.get_global_rank(self.pg, 0) if self.pg is not dist.group.WORLD else 0,
+                           group=self.pg)
 
     def _make_bucketer(self):
         flags = L.GS_BKT_NO_UNPACK
@@ -179,6 +215,10 @@ class ZeroDataParallel:
             L.gs_dtype(self.dtype), BUCKET_ALIGN_ELEMS, float(self.world), flags, ctypes.byref(h)),
             "gs_bucketer_create")
         self.handle = h
+        if self.is_cuda:
+            # no tail timing on the ZeRO engine: its end-of-backward chain records no
+            # event packets (~4.7 µs of stream time each)
+            L.check(L.lib().gs_bucketer_set_timeline(h, 0), "gs_bucketer_set_timeline")
         if self._comm is not None:
             self._comm.add_user(self)
         self._ready = (ctypes.c_int32 * max(1, len(self.buckets)))()
@@ -336,11 +376,69 @@ class ZeroDataParallel:
     def _allreduce_scalar(self, t, op):
         if self._comm is not None:
             self._comm.all_reduce(t, op=op, stream=L.stream_ptr(self.device))
+            return
+        rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+        if self._host_staged(t):
+            host = t.cpu()
+            dist.all_reduce(host, op=rop, group=self.pg)
+            t.copy_(host)
         else:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=self.pg)
+            dist.all_reduce(t, op=rop, group=self.pg)
+
+    # ---- overlapped parameter all-gather (opt-in, overlap_allgather)
+    def _launch_allgathers(self):
+        """Each bucket's in-place all-gather behind the update, last bucket (the
+        model's first layers, needed first by the next forward) first; on the
+        communicator's stream when there is one, so the next forward's early layers
+        run while the later buckets travel."""
+        order = list(reversed(range(len(self.param_flats))))
+        if self._comm is not None:
+            cs = self._comm.stream
+            cs.wait_stream(torch.cuda.current_stream(self.device))  # the update wrote this rank's slices
+            for b in order:
+                flat = self.param_flats[b]
+                shard = flat[self.rank * self.shard_sizes[b]:(self.rank + 1) * self.shard_sizes[b]]
+                self._comm.all_gather(shard, flat, stream=self._comm.stream_ptr)
+                self._ag_ev[b].record(cs)
+        else:
+            for b in order:  # the process group: synchronous, the events mark the same points
+                self._all_gather_flat(b, self.param_flats[b])
+                if self._ag_ev[b] is not None:
+                    self._ag_ev[b].record()
+        self._ag_pending = set(order)
+
+    def _wait_buckets(self, buckets):
+        if not self._ag_pending:
+            return
+        for b in buckets:
+            if b in self._ag_pending:
+                self._ag_pending.discard(b)
+                if self._ag_ev[b] is not None:
+                    torch.cuda.current_stream(self.device).wait_event(self._ag_ev[b])
+
+    def wait_allgather(self):
+        """Order the current stream after every pending parameter all-gather
+        (overlap_allgather): what a module's forward pre-hook does for its own
+        parameters; call it before reading parameters outside a forward."""
+        self._wait_buckets(sorted(self._ag_pending))
+
+    def time_allgather(self, on: bool = True):
+        """HIP events around the end-of-step all-gathers on the step's stream
+        (the exposed all-gather: all of it by default, the issue cost with
+        overlap_allgather); :meth:`last_allgather_ms` reads the last step's."""
+        self._ag_time = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
+            if on and self.is_cuda else None
+
+    def last_allgather_ms(self):
+        t = self._ag_time
+        if t is None:
+            return None
+        t[1].synchronize()
+        return t[0].elapsed_time(t[1])
 
     @torch.no_grad()
     def step(self):
+        self.wait_allgather()  # the update writes this rank's slice of the parameter buffers
         s = self._scratch
         found_inf = None
         grad_scale = None
@@ -360,14 +458,20 @@ class ZeroDataParallel:
                 self.plan.sqnorm_partial(1, self.dtype)
                 self.plan.set_clip(self.clip, 1e-6, None, inv_scale * inv_scale, inv_scale, out=s[4:7])
             else:
-                # this shard's group sums (<= 64 floats) SUM-all-reduced over the ranks (one
-                # message, identical bits everywhere), folded by every update workgroup:
-                # Σg² kernel -> 256-B collective -> update, nothing in between (DeepSpeed:
-                # per-rank Σ, scalar all_reduce, coefficient, U)
+                # this shard's Σg² partial sums (a small shard, e.g. ResNet-50 at N=8: one per
+                # workgroup of a <= 512-workgroup grid, no in-kernel combine) SUM-all-reduced
+                # over the ranks (one 2 KiB message, identical bits everywhere), folded by
+                # every update workgroup: Σg² kernel -> collective -> update, nothing in
+                # between (DeepSpeed: per-rank Σ, scalar all_reduce, coefficient, U).
+                # The whole buffer travels and is folded: the slots past this rank's count
+                # stay zero and add nothing (clip_multiplier folds absent partials as 0.f,
+                # so the bits do not depend on n), and the message length never depends on
+                # a rank's own grid
                 gr = self._red_groups
-                n = self.plan.sqnorm_partial_out(1, self.dtype, gr)
-                self._allreduce_scalar(gr[:n], "sum")
-                self.plan.set_clip_groups(self.clip, 1e-6, gr, n, inv_scale * inv_scale, inv_scale, out=s[4:7])
+                self.plan.sqnorm_partial_out(1, self.dtype, gr)
+                self._allreduce_scalar(gr, "sum")
+                self.plan.set_clip_groups(self.clip, 1e-6, gr, gr.numel(), inv_scale * inv_scale, inv_scale,
+                                          out=s[4:7])
         elif self.clip > 0:
             self.plan.set_clip(None)
             sq = s[1:2]
@@ -407,8 +511,16 @@ class ZeroDataParallel:
                            (g0["lr"] / bc1) * -1, bc2 ** 0.5, lowp_dtype=lowp, grad_scale=grad_scale,
                            found_inf=found_inf)
         # re-replicate the updated parameters: in-place all-gather per bucket
-        for b, flat in enumerate(self.param_flats):
-            self._all_gather_flat(b, flat)
+        t = self._ag_time
+        if t is not None:
+            t[0].record()
+        if self.overlap_allgather:
+            self._launch_allgathers()
+        else:
+            for b, flat in enumerate(self.param_flats):
+                self._all_gather_flat(b, flat)
+        if t is not None:
+            t[1].record()
         overflow = False
         if self.scaler is not None:
             overflow = bool(found_inf.item() != 0)  # DeepSpeed reads the overflow flag on the host
@@ -465,6 +577,7 @@ class ZeroDataParallel:
     @torch.no_grad()
     def load_state_dict(self, sd):
         """Restore this rank's shard (same world size and bucket layout)."""
+        self.wait_allgather()
         if sd["world"] != self.world or sd["rank"] != self.rank or list(sd["bucket_numel"]) != self.bucket_numel:
             raise RuntimeError(f"ZeRO checkpoint shard is for rank {sd['rank']}/{sd['world']} with buckets "
                                f"{sd['bucket_numel']}; this engine is rank {self.rank}/{self.world} with "
@@ -491,6 +604,10 @@ class ZeroDataParallel:
         shard = flat[self.rank * self.shard_sizes[b]:(self.rank + 1) * self.shard_sizes[b]]
         if self._comm is not None:
             self._comm.all_gather(shard, flat, stream=L.stream_ptr(self.device))
+        elif self._host_staged(flat):
+            host = torch.empty(flat.numel(), dtype=flat.dtype)
+            dist.all_gather(list(host.chunk(self.world)), shard.cpu(), group=self.pg)
+            flat.copy_(host)
         else:
             chunks = list(flat.chunk(self.world))
             dist.all_gather(chunks, shard.clone(), group=self.pg)
@@ -507,6 +624,10 @@ class ZeroDataParallel:
             full = torch.empty(self.bucket_numel[b], dtype=torch.float32, device=self.device)
             if self._comm is not None:
                 self._comm.all_gather(m.contiguous(), full, stream=L.stream_ptr(self.device))
+            elif self._host_staged(full):
+                host = torch.empty(full.numel(), dtype=full.dtype)
+                dist.all_gather(list(host.chunk(self.world)), m.contiguous().cpu(), group=self.pg)
+                full.copy_(host)
             else:
                 dist.all_gather(list(full.chunk(self.world)), m.contiguous(), group=self.pg)
             fulls.append(full)
@@ -526,6 +647,7 @@ class ZeroDataParallel:
         """Inverse of :meth:`consolidated_state_dict`: fp32 values into the master
         shards and the (low-precision) model, buffers into the module.  No
         collective: every rank reads the full dict."""
+        self.wait_allgather()
         names = {id(p): n for n, p in self.module.named_parameters()}
         fulls = [torch.zeros(n, dtype=torch.float32, device=self.device) for n in self.bucket_numel]
         for i, p in enumerate(self.params):
@@ -544,9 +666,11 @@ class ZeroDataParallel:
                                f"unexpected {unexpected}")
 
     def close(self):
-        for h in self._hooks:
+        self.wait_allgather()
+        for h in self._hooks + getattr(self, "_ag_hooks", []):
             h.remove()
         self._hooks = []
+        self._ag_hooks = []
         nat = getattr(self, "_native", None)
         if nat is not None:
             nat.detach()

@@ -230,25 +230,32 @@ int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream);
  *           DeepSpeed gradient_clipping (R:resnet/deepspeed/deepspeed_train.py:195) */
 int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
                      float coef_mul, float* out_dev);
-/* The group sums of the fused Σx² reduction, written out: gs_sqnorm_partial's
- * kernel, which also stores its group sums contiguously to groups_out (device
- * memory of the plan's kind, GS_RED_GROUPS floats); *n_groups (host) receives
- * how many are valid, 1..GS_RED_GROUPS (1: a finished Σ, e.g. host plans or a
- * reduction configured without the in-kernel combine).  A sharded optimizer
- * SUM-all-reduces these n floats across its ranks (one message of <= 256 B,
- * identical bits on every rank) and hands them to gs_plan_set_clip_groups: the
- * global ‖g‖ of every shard with no combine launch and no scalar
- * coefficient launch on the step's exposed end.
+/* The partial sums of Σx² over the plan, written out for a sharded optimizer:
+ * groups_out (device memory of the plan's kind) must hold GS_RED_PARTIALS
+ * floats; *n_groups (host) receives how many are valid, 1..GS_RED_PARTIALS.
+ * A plan of at most 2 Ki chunk groups (a ZeRO shard at N = 8: 3.2 M elements)
+ * writes one partial per workgroup of a balanced grid of <= GS_RED_PARTIALS
+ * workgroups — no arrival counters, no in-kernel combine, nothing after the
+ * streaming but one store per workgroup; a larger plan writes the fused
+ * reduction's <= 64 group sums (gs_sqnorm_partial's kernel); 1 = a finished Σ
+ * (host plans, a reduction without the in-kernel combine).  A sharded
+ * optimizer SUM-all-reduces the whole GS_RED_PARTIALS-float buffer across its
+ * ranks (slots past n stay zero and fold as zero, so the message never depends
+ * on a rank's own grid) and hands it to gs_plan_set_clip_groups: the global ‖g‖
+ * of every shard with no combine launch and no scalar coefficient launch on the
+ * step's exposed end.
  * replaces: DeepSpeed stage_1_and_2 get_grad_norm_direct (per-rank Σg² of the
  *           partition, all_reduce of the scalar, U) for gradient_clipping
  *           (R:resnet/deepspeed/deepspeed_train.py:195) */
 #define GS_RED_GROUPS 64
+#define GS_RED_PARTIALS 512
 int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, int32_t* n_groups,
                           void* stream);
-/* gs_plan_set_clip with ‖g‖² = the fold of n_groups partial sums at groups_dev
- * (contiguous; typically gs_sqnorm_partial_out's, summed over ranks): every
- * update workgroup folds them with the fused reduction's own last step (a
- * fixed 64-lane tree), so every rank forms the same coefficient. */
+/* gs_plan_set_clip with ‖g‖² = the fold of n_groups (<= GS_RED_PARTIALS)
+ * partial sums at groups_dev (contiguous; typically gs_sqnorm_partial_out's,
+ * summed over ranks): every update workgroup folds them in a fixed order —
+ * lane l of one wave adds partials l, l + 64, l + 128, ..., then the fused
+ * reduction's own 64-lane tree — so every rank forms the same coefficient. */
 int gs_plan_set_clip_groups(gs_plan* p, const float* groups_dev, int32_t n_groups, float max_norm,
                             float eps, float sq_mul, float coef_mul, float* out_dev);
 /* coef_dev[0] = min(1, max_norm / (sqrt(sqnorm_dev[0]) + eps)); norm_dev (nullable) = sqrt

@@ -68,7 +68,11 @@ def _bf16_np(t: torch.Tensor) -> np.ndarray:
     return t.detach().float().cpu().numpy().reshape(-1)
 
 
-def ds_step_vs_oracle(rank, ws, dev, kind="micro", steps=3):
+def ds_step_vs_oracle(rank, ws, dev, kind="micro", steps=3, overlap=False):
+    """overlap: ZeroDataParallel(overlap_allgather=True) — several buckets, the
+    parameter all-gathers issued behind the update on the communicator's stream
+    and awaited before the parameters are read (wait_allgather: this synthetic
+    loss reads them outside any module forward)."""
     from distributed_training_amd.zero import ZeroDataParallel, warmup_lr
     from oracle import oracle as O
 
@@ -80,7 +84,10 @@ def ds_step_vs_oracle(rank, ws, dev, kind="micro", steps=3):
     for i, p in enumerate(params):  # the local grads before the pack (registered before ZeRO's hooks)
         p.register_post_accumulate_grad_hook(lambda q, i=i: local.__setitem__(i, _bf16_np(q.grad)))
     z = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=LR_MAX, betas=BETAS, eps=EPS, weight_decay=WD,
-                         reduce_bucket_size=int(5e7), gradient_clipping=CLIP)
+                         reduce_bucket_size=int(5e7), gradient_clipping=CLIP, overlap_allgather=overlap,
+                         allgather_bucket_size=max(1000, n_total // 5) if overlap else None)
+    if overlap:
+        assert len(z.buckets) >= 3, len(z.buckets)
     master_o = [_bf16_np(p).copy() for p in params]
     m_o = [np.zeros_like(x) for x in master_o]
     v_o = [np.zeros_like(x) for x in master_o]
@@ -101,9 +108,11 @@ def ds_step_vs_oracle(rank, ws, dev, kind="micro", steps=3):
         rs = [torch.randn(p.shape, device=dev, generator=g) * sigma for p in params]
         local.clear()
         z.prepare_backward()
+        z.wait_allgather()  # the loss below reads the parameters outside a module forward
         loss = sum((p.float() * r).sum() for p, r in zip(params, rs))
         loss.backward()
         z.step()
+        z.wait_allgather()
         if dev.type == "cuda":
             torch.cuda.synchronize()
         assert len(local) == len(params)
@@ -164,6 +173,40 @@ def ds_step_vs_oracle(rank, ws, dev, kind="micro", steps=3):
     z.close()
 
 
+def overlap_matches_default(rank, ws, dev, steps=3):
+    """overlap_allgather through real module forwards (the forward pre-hooks wait
+    for each bucket's all-gather): weights bit-identical to the default engine's
+    after every step (clip off: the clip's Σg² partition follows the bucket
+    layout, so with a clip the two agree to fp32 rounding, the oracle test above
+    pins that path)."""
+    from distributed_training_amd.resnet import BasicBlock, ResNet
+    from distributed_training_amd.zero import ZeroDataParallel
+
+    out = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        model = ResNet(BasicBlock, [1, 1, 1, 1], num_classes=10, width=8).to(dev).to(torch.bfloat16)
+        z = ZeroDataParallel(model, stage=2, optimizer="adamw", lr=1e-2, betas=BETAS, eps=EPS, weight_decay=WD,
+                             overlap_allgather=overlap, allgather_bucket_size=20000 if overlap else None)
+        assert (len(z.buckets) > 2) == overlap
+        g = torch.Generator(device=dev).manual_seed(50 + rank)
+        ws_seen = []
+        for it in range(steps):
+            x = torch.rand(4, 3, 32, 32, device=dev, generator=g).to(torch.bfloat16)
+            y = torch.randint(0, 10, (4,), device=dev, generator=g)
+            z.prepare_backward()
+            torch.nn.functional.cross_entropy(model(x).float(), y).backward()
+            z.step()
+            if overlap and dev.type == "cuda" and z._comm is not None:
+                assert z._ag_pending, "the all-gathers are left in flight for the next forward"
+            z.wait_allgather()
+            ws_seen.append(torch.cat([p.detach().float().reshape(-1).cpu() for p in model.parameters()]))
+        z.close()
+        out.append(ws_seen)
+    for it, (a, b) in enumerate(zip(*out)):
+        assert torch.equal(a, b), f"step {it}: overlap_allgather changed the weights"
+
+
 # ---------------------------------------------------------------- CPU (gloo)
 @pytest.mark.parametrize("ws", [2, 3])
 def test_ds_zero2_clip_step_vs_oracle_cpu(ws):
@@ -174,6 +217,17 @@ def test_ds_zero2_clip_step_vs_oracle_cpu(ws):
 
 def _cpu_worker(rank, ws):
     ds_step_vs_oracle(rank, ws, torch.device("cpu"), "micro")
+
+
+def test_ds_zero2_overlap_allgather_cpu_ws2():
+    from tests.test_ddp_cpu import _run
+
+    _run(_cpu_overlap_worker, 2)
+
+
+def _cpu_overlap_worker(rank, ws):
+    ds_step_vs_oracle(rank, ws, torch.device("cpu"), "micro", overlap=True)
+    overlap_matches_default(rank, ws, torch.device("cpu"))
 
 
 # ---------------------------------------------------------------- GPU
@@ -197,12 +251,27 @@ def test_ds_zero2_clip_step_vs_oracle_resnet50_ws1_rccl(cuda_device, rccl_pg):
     ds_step_vs_oracle(0, 1, cuda_device, "resnet50")
 
 
-def _gpu_ws2_worker(rank, ws, port, errq):
+@pytest.mark.gpu
+def test_ds_zero2_overlap_allgather_ws1_rccl(cuda_device, rccl_pg):
+    """overlap_allgather over RCCL: the all-gathers run on the communicator's stream
+    behind the update and are awaited by the next forward's modules — the oracle
+    chain bit for bit on ResNet-50's parameters, and the same weights as the
+    default engine through real forwards (deterministic MIOpen)."""
+    ds_step_vs_oracle(0, 1, cuda_device, "resnet50", overlap=True)
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        overlap_matches_default(0, 1, cuda_device)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+
+
+def _gpu_ws2_worker(rank, ws, port, errq, overlap=False):
     try:
         init_pg("gloo", rank, ws, port)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        ds_step_vs_oracle(rank, ws, dev, "resnet50")
+        ds_step_vs_oracle(rank, ws, dev, "resnet50", overlap=overlap)
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:
@@ -213,14 +282,16 @@ def _gpu_ws2_worker(rank, ws, port, errq):
 
 
 @pytest.mark.gpu
-def test_ds_zero2_clip_step_vs_oracle_resnet50_ws2_one_gpu(cuda_device):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_ds_zero2_clip_step_vs_oracle_resnet50_ws2_one_gpu(cuda_device, overlap):
     """The world > 1 branch (zero.py: group sums of each shard, one SUM
-    all-reduce of <= 64 floats, the update folding them) with HIP plans: two
-    ranks sharing the box's GPU, gloo carrying the collectives."""
+    all-reduce of 64 floats, the update folding them) with HIP plans: two
+    ranks sharing the box's GPU, gloo carrying the collectives; and the same
+    with overlap_allgather (several buckets, per-bucket gathers)."""
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_gpu_ws2_worker, args=(r, 2, port, errq)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_ws2_worker, args=(r, 2, port, errq, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
