@@ -214,7 +214,12 @@ class DeepSpeedEngine(nn.Module):
                 self.module, stage=max(1, stage), optimizer=kind, lr=lr, betas=betas, eps=eps, weight_decay=wd,
                 momentum=p.get("momentum", 0.0), reduce_bucket_size=int(zcfg.get("reduce_bucket_size", 5e8)
                                                                       if isinstance(zcfg, dict) else 5e8),
-                gradient_clipping=self.clip, loss_scaler=scaler)
+                gradient_clipping=self.clip, loss_scaler=scaler,
+                # libgsync extension keys (DeepSpeed ignores unknown ones): per-bucket parameter
+                # all-gathers under the next forward instead of DeepSpeed's end-of-step gather
+                overlap_allgather=bool(isinstance(zcfg, dict) and zcfg.get("overlap_allgather", False)),
+                allgather_bucket_size=(zcfg.get("overlap_allgather_bucket_size") if isinstance(zcfg, dict)
+                                       else None))
             self.optimizer = self._zero
         else:
             self._ddp = DistributedDataParallel(self.module, broadcast_buffers=False)

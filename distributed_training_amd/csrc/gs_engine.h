@@ -729,10 +729,11 @@ __device__ __forceinline__ char* flat_at(void* flat, int64_t off) {
 // left a uniform branch and the unused IEEE-division path inside every
 // lane-step of the streaming loop
 // NT: non-temporal loads of the source (a read-once stream above the cache size, nt_read_once)
-template <int N, int SD, int FD, int MODE, bool NT = false>
+// G2: a small plan into an fp32 bucket takes groups of 2 chunks (pack_group_small)
+template <int N, int SD, int FD, int MODE, bool NT = false, bool G2 = false>
 struct PackOp {
   static constexpr int kN = N;
-  static constexpr int kG = FD == GS_F32 ? GS_G_PACK : (SD == GS_F32 ? GS_G_PACK16 : GS_G_PACK16_16);
+  static constexpr int kG = FD == GS_F32 ? (G2 ? 2 : GS_G_PACK) : (SD == GS_F32 ? GS_G_PACK16 : GS_G_PACK16_16);
   static constexpr int kRed = 0;
   static constexpr int kRedGrid = kGridLimit;
   static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
@@ -1058,10 +1059,21 @@ __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float*
   float sq;
   if (c.groups > 0) {
     // lane l: partials l, l + 64, ... in order (<= GS_RED_PARTIALS), then the tree;
-    // for <= 64 group sums exactly the fused combine's last step
+    // for <= 64 group sums exactly the fused combine's last step.  All loads are
+    // issued before the first add (one memory round trip per workgroup, not one per
+    // partial: a serial loop here cost the update 1.4 µs, profiles/r5/r5c_rows.jsonl);
+    // an absent partial adds +0 (the partials are sums of squares: never -0)
+    constexpr int kPer = GS_RED_PARTIALS / 64;
     const int l = static_cast<int>(threadIdx.x & 63);
+    float v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int j = l + 64 * k;
+      v[k] = j < c.groups ? c.sq[j * c.stride] : 0.f;
+    }
     float x = 0.f;
-    for (int j = l; j < c.groups; j += 64) x = x + c.sq[j * c.stride];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) x = x + v[k];
     sq = wave_sum(0.f + x);
   } else {
     sq = c.sq[0];

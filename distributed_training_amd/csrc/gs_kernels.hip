@@ -223,8 +223,23 @@ int hip_plan_flush(gs_plan* p, void* stream) {
 }
 
 // ------------------------------------------------------------- dispatchers
+// An fp32 bucket whose plan fits one resident wave at groups of 2 chunks (<= 4 Ki
+// chunks, 16 MB of fp32: the exposed last DDP bucket, ResNet-50's 9.7 MB) takes
+// groups of 2 — half the workgroups, two accesses in flight per lane — where the
+// large buckets keep one chunk per workgroup (the dispatcher refills CUs faster
+// than a resident grid loops).  Level-2 tail, two rounds: pack 7.6-7.8 -> 7.0-7.2
+// µs, the tail 35.9-36.8 -> 34.8-34.9 µs (profiles/r5/r5c_rows.jsonl, variant gpack2).
+constexpr int64_t kPackG2MaxChunks = 4096;
+
 template <int SD, int FD, int MODE, bool NT>
 static int pack_mode(gs_plan* p, int src_slot, void* flat, float s, void* stream) {
+  if constexpr (FD == GS_F32) {
+    if (static_cast<int64_t>(p->chunks.size()) <= kPackG2MaxChunks) {
+      PackOp<kUnit, SD, FD, MODE, NT, true> op;
+      op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s;
+      return launch(p, op, stream);
+    }
+  }
   PackOp<kUnit, SD, FD, MODE, NT> op;
   op.slot = src_slot; op.flat = flat; op.flat_vec = flat_aligned(flat); op.s = s;
   return launch(p, op, stream);

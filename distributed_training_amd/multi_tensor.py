@@ -191,6 +191,8 @@ class TensorListPlan:
                 raise ValueError("clip tensors: fp32, where the plan runs")
         if out is not None and out.numel() < 3:
             raise ValueError("clip out: 3 elements")
+        if not groups.is_contiguous() or groups.numel() < int(n_groups):
+            raise ValueError(f"partial sums: {n_groups} contiguous floats expected, got {groups.numel()}")
         L.check(L.lib().gs_plan_set_clip_groups(self.handle, groups.data_ptr(), int(n_groups), float(max_norm or 0.0),
                                                 float(eps), float(sq_mul), float(coef_mul),
                                                 None if out is None else out.data_ptr()), "gs_plan_set_clip_groups")

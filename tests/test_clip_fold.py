@@ -167,13 +167,20 @@ def test_plan_clip_partial_is_single_use():
 
 
 def _dpp_wave_sum(x):
-    """The update kernel's 64-lane fold (gs_kernels.hip wave_reduce), restated
-    independently: quad_perm [1,0,3,2] / [2,3,0,1] and the half-row / row
-    mirrors are lane XORs 1 / 2 / 7 / 15; row_bcast:15 adds lane 15 of the row
-    below into rows 1 and 3, row_bcast:31 adds lane 31 into rows 2 and 3."""
+    """The update kernel's fold of up to 512 partial sums (gs_engine.h
+    clip_multiplier), restated independently: lane l first adds partials l,
+    l + 64, ... in order (fp32), then the 64-lane tree of wave_reduce —
+    quad_perm [1,0,3,2] / [2,3,0,1] and the half-row / row mirrors are lane XORs
+    1 / 2 / 7 / 15; row_bcast:15 adds lane 15 of the row below into rows 1 and 3,
+    row_bcast:31 adds lane 31 into rows 2 and 3."""
     lanes = np.arange(64)
     v = np.zeros(64, np.float32)
-    v[:len(x)] = np.asarray(x, np.float32)
+    x = np.asarray(x, np.float32)
+    for lane in range(64):
+        a = np.float32(0.0)
+        for j in range(lane, len(x), 64):
+            a = np.float32(a + x[j])
+        v[lane] = a
 
     def step(v, src, rows):
         t = np.zeros(64, np.float32)
@@ -188,12 +195,12 @@ def _dpp_wave_sum(x):
     return v[63]
 
 
-@pytest.mark.parametrize("n", [1, 5, 64])
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 200, 512])
 def test_clip_groups_fold_host(n):
     """gs_plan_set_clip_groups on a host plan: the published Σg² is the device
-    fold of the group sums (restated above), coefficient and update follow."""
+    fold of the partial sums (restated above), coefficient and update follow."""
     g0 = torch.Generator().manual_seed(n)
-    groups = torch.rand(64, generator=g0) * 100.0
+    groups = torch.rand(D._lib.GS_RED_PARTIALS, generator=g0) * 100.0
     plan = D.multi_tensor.TensorListPlan([16], torch.device("cpu"), task_units=0)
     p, g, b = torch.zeros(16), torch.ones(16), torch.zeros(16)
     for k, t in enumerate((p, g, b)):
@@ -209,7 +216,9 @@ def test_clip_groups_fold_host(n):
     want = np.float32(-0.1) * np.float32(np.float32(1.0) * coef)  # fmaf(-lr, g·coef, 0)
     assert torch.equal(p, torch.full((16,), float(want)))
     with pytest.raises(D._lib.GsyncError, match="n_groups"):
-        plan.set_clip_groups(1.0, 1e-6, groups, 65)
+        plan.set_clip_groups(1.0, 1e-6, torch.zeros(1024), D._lib.GS_RED_PARTIALS + 1)
+    with pytest.raises(ValueError, match="partial sums"):
+        plan.set_clip_groups(1.0, 1e-6, groups[:8], 9)
 
 
 def test_sqnorm_partial_out_host():
@@ -217,11 +226,13 @@ def test_sqnorm_partial_out_host():
     xs = [torch.randn(n, generator=torch.Generator().manual_seed(n)) for n in (7, 1000, 33)]
     plan = D.multi_tensor.TensorListPlan([x.numel() for x in xs], torch.device("cpu"), task_units=0)
     plan.set_ptrs(1, xs)
-    gr = torch.zeros(64)
+    gr = torch.zeros(D._lib.GS_RED_PARTIALS)
     n = plan.sqnorm_partial_out(1, torch.float32, gr)
     ref = torch.zeros(1)
     plan.sqnorm(1, torch.float32, ref)
     assert n == 1 and gr[0].item() == ref.item()
+    with pytest.raises(ValueError, match="partial sums"):
+        plan.sqnorm_partial_out(1, torch.float32, torch.zeros(64))
 
 
 @pytest.mark.gpu
@@ -274,11 +285,13 @@ def test_folded_clip_large_plan_gpu(mixed):
 @pytest.mark.gpu
 def test_clip_groups_fold_gpu_equals_host_and_sqnorm():
     """The device fold of gs_plan_set_clip_groups == the host restatement bit for
-    bit (64, 5 and 1 random group sums); gs_sqnorm_partial_out's group sums of a
-    ResNet-50-sized slot folded == gs_sqnorm's Σg² bit for bit."""
+    bit (512, 200, 65, 64, 5 and 1 random partial sums); gs_sqnorm_partial_out's
+    64 group sums of a large slot folded == gs_sqnorm's Σg² bit for bit; on a
+    small plan (a ZeRO N=8 shard) its raw per-workgroup partials, folded, equal
+    the restated fold of the same partials and the double Σ to fp32 rounding."""
     dev = torch.device("cuda", 0)
-    for n in (64, 5, 1):
-        groups = torch.rand(64, generator=torch.Generator().manual_seed(n)) * 100.0
+    for n in (512, 200, 65, 64, 5, 1):
+        groups = torch.rand(D._lib.GS_RED_PARTIALS, generator=torch.Generator().manual_seed(n)) * 100.0
         outs = []
         for d in (dev, torch.device("cpu")):
             plan = D.multi_tensor.TensorListPlan([4096], d, task_units=0)
@@ -296,13 +309,32 @@ def test_clip_groups_fold_gpu_equals_host_and_sqnorm():
     xs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
     plan = D.multi_tensor.TensorListPlan(sizes, dev)
     plan.set_ptrs(1, xs)
-    gr = torch.zeros(64, device=dev)
+    gr = torch.zeros(D._lib.GS_RED_PARTIALS, device=dev)
     n = plan.sqnorm_partial_out(1, torch.float32, gr)
     ref = torch.zeros(1, device=dev)
     plan.sqnorm(1, torch.float32, ref)
     torch.cuda.synchronize()
     assert n == 64
     assert float(np.float32(_dpp_wave_sum(gr.cpu().numpy()[:n]))) == ref.item()
+    # the raw form: 3.2 M bf16 elements (ResNet-50 / 8), one partial per workgroup
+    shard = (torch.randn(3194688, device=dev, generator=gen) * 1e-3).to(torch.bfloat16)
+    small = D.multi_tensor.TensorListPlan([shard.numel()], dev)
+    small.set_ptrs(1, [shard])
+    gr.zero_()
+    n = small.sqnorm_partial_out(1, torch.bfloat16, gr)
+    torch.cuda.synchronize()
+    parts = gr.cpu().numpy()
+    assert 64 < n <= D._lib.GS_RED_PARTIALS and not parts[n:].any(), n
+    exact = float((shard.double() ** 2).sum())
+    assert abs(float(parts[:n].astype(np.float64).sum()) - exact) <= 1e-5 * exact
+    p1, g1, b1 = (torch.zeros(8, device=dev), torch.ones(8, device=dev), torch.zeros(8, device=dev))
+    up = D.multi_tensor.TensorListPlan([8], dev)
+    for k, t in enumerate((p1, g1, b1)):
+        up.set_ptrs(k, [t])
+    out = torch.zeros(3, device=dev)
+    up.set_clip_groups(1.0, 1e-6, gr, n, out=out)
+    up.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+    assert out[0].item() == float(np.float32(_dpp_wave_sum(parts[:n])))
 
 
 _RED_FUSE_CHILD = r"""
