@@ -850,11 +850,12 @@ struct ScaleOp {
 };
 
 // NT: non-temporal loads (a read-once stream larger than the Infinity Cache,
-// nt_read_once below)
-template <int N, int DT, bool NT = false>
+// nt_read_once below).  G: chunks per group (the raw partials of a small plan take
+// 8: one group per workgroup, every access of the workgroup in flight at once)
+template <int N, int DT, bool NT = false, int G = GS_G_RED>
 struct SqnormOp {
   static constexpr int kN = N;
-  static constexpr int kG = GS_G_RED;
+  static constexpr int kG = G;
   static constexpr int kRed = 1;
   static constexpr int kRedGrid = 8192;
   static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
@@ -1150,7 +1151,8 @@ struct DeviceGuard {
 // sums, which stay in the plan for the next clipped update (p->red_groups);
 // groups_only = 2 (raw, gs_sqnorm_partial_out on a small plan): a balanced grid of
 // <= GS_RED_PARTIALS workgroups, each writing its partial to red_out
-constexpr int kRawGroupsMax = 2048;  // chunk groups up to which the raw form serves
+constexpr int kRawG = 8;  // chunks per group of the raw form: one group per workgroup
+constexpr int64_t kRawChunksMax = static_cast<int64_t>(kRawG) * GS_RED_PARTIALS;  // plans it serves
 template <class Op>
 int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0,
            int groups_only = 0) {

@@ -310,6 +310,15 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
 
 template <bool NT>
 static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
+  if (groups_only == 2) {
+    // raw partials of a small plan: groups of 8 chunks, one per workgroup (<= 512 of them)
+    GS_DISPATCH_FLOAT(dt, DT, {
+      SqnormOp<kUnit, DT, NT, kRawG> op;
+      op.slot = slot;
+      return launch(p, op, stream, sq, acc, groups_only);
+    });
+    return GS_OK;
+  }
   GS_DISPATCH_FLOAT(dt, DT, {
     SqnormOp<kUnit, DT, NT> op;
     op.slot = slot;
@@ -349,10 +358,11 @@ float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit
 // also contiguous in caller memory, or the finished Σ in groups_out[0].
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream) {
   DeviceGuard g(p->device);
-  // caller memory on a small plan (a ZeRO shard at N = 8): one partial per workgroup of a
-  // balanced grid, no counters and no combine — the kernel ends with its last store
-  const int64_t chunk_groups = (static_cast<int64_t>(p->chunks.size()) + GS_G_RED - 1) / GS_G_RED;
-  if (groups_out && !p->chunks.empty() && p->n > 0 && !p->segs.empty() && chunk_groups <= kRawGroupsMax) {
+  // caller memory on a small plan (<= 4 Ki chunks: a ZeRO shard at N = 8): one partial per
+  // workgroup, each streaming one group of 8 chunks with all its loads in flight at once,
+  // no counters and no combine — the kernel ends with its last store
+  if (groups_out && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
+      static_cast<int64_t>(p->chunks.size()) <= kRawChunksMax) {
     GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 2, stream));
     if (n_groups) *n_groups = p->red_groups;
     return GS_OK;

@@ -5,8 +5,8 @@
 // event pair around the chain.  Variants: plain launches; each launch followed
 // by hipEventRecord of a timing-disabled event (what every plan launch did to
 // keep `last_event`); of a timing event; the same event attached to the launch
-// itself (hipExtLaunchKernel's stop event); a cross-stream wait on an event
-// recorded long before.  Kernels: a 1-workgroup no-op (pure dispatch) and a
+// itself (hipExtLaunchKernel's stop event; its start event; both); a
+// cross-stream wait on an event recorded long before.  Kernels: a 1-workgroup no-op (pure dispatch) and a
 // 12.8 MB copy (3.2 M floats: a ZeRO N=8 shard).  One JSON line per case.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -39,9 +39,10 @@ __global__ void __launch_bounds__(256) copy4(const f4* __restrict__ x, f4* __res
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) y[i] = x[i];
 }
 
-enum Mode { PLAIN = 0, REC_NOTIME = 1, REC_TIME = 2, EXT_NOTIME = 3, EXT_TIME = 4, XWAIT = 5 };
+enum Mode { PLAIN = 0, REC_NOTIME = 1, REC_TIME = 2, EXT_NOTIME = 3, EXT_TIME = 4, XWAIT = 5, EXT_START = 6,
+            EXT_BOTH = 7 };
 static const char* kModeName[] = {"plain", "record_notiming", "record_timing", "ext_stop_notiming",
-                                  "ext_stop_timing", "cross_stream_wait"};
+                                  "ext_stop_timing", "cross_stream_wait", "ext_start_timing", "ext_start_stop_timing"};
 
 int main() {
   hipStream_t s, s2;
@@ -54,12 +55,13 @@ int main() {
   CK(hipMalloc(&tiny, 64));
   CK(hipMemset(x, 0, n * 4));
   CK(hipMemset(tiny, 0, 64));
-  hipEvent_t a, b, ev_nt, ev_t, ev_x;
+  hipEvent_t a, b, ev_nt, ev_t, ev_x, ev_s;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   CK(hipEventCreateWithFlags(&ev_nt, hipEventDisableTiming));
   CK(hipEventCreate(&ev_t));
   CK(hipEventCreateWithFlags(&ev_x, hipEventDisableTiming));
+  CK(hipEventCreate(&ev_s));
   // spin calibration: ~150 us of clock64 at any clock
   hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, s, 1000000LL);
   CK(hipEventRecord(a, s));
@@ -72,7 +74,7 @@ int main() {
   const int grid_copy = 2048;
   for (int kernel = 0; kernel < 2; ++kernel) {
     for (int K : {1, 3}) {
-      for (int mode = 0; mode < 6; ++mode) {
+      for (int mode = 0; mode < 8; ++mode) {
         std::vector<float> t;
         for (int it = 0; it < 60; ++it) {
           CK(hipEventRecord(ev_x, s2));  // long done by the time s reaches its wait
@@ -80,13 +82,14 @@ int main() {
           CK(hipEventRecord(a, s));
           for (int k = 0; k < K; ++k) {
             if (mode == XWAIT) CK(hipStreamWaitEvent(s, ev_x, 0));
-            hipEvent_t stop = mode == EXT_NOTIME ? ev_nt : mode == EXT_TIME ? ev_t : nullptr;
+            hipEvent_t stop = mode == EXT_NOTIME ? ev_nt : (mode == EXT_TIME || mode == EXT_BOTH) ? ev_t : nullptr;
+            hipEvent_t start = (mode == EXT_START || mode == EXT_BOTH) ? ev_s : nullptr;
             if (kernel == 0) {
-              if (stop) hipExtLaunchKernelGGL(noop, dim3(1), dim3(64), 0, s, nullptr, stop, 0, tiny);
+              if (stop || start) hipExtLaunchKernelGGL(noop, dim3(1), dim3(64), 0, s, start, stop, 0, tiny);
               else hipLaunchKernelGGL(noop, dim3(1), dim3(64), 0, s, tiny);
             } else {
-              if (stop)
-                hipExtLaunchKernelGGL(copy4, dim3(grid_copy), dim3(256), 0, s, nullptr, stop, 0, (const f4*)x,
+              if (stop || start)
+                hipExtLaunchKernelGGL(copy4, dim3(grid_copy), dim3(256), 0, s, start, stop, 0, (const f4*)x,
                                       (f4*)y, n / 4);
               else
                 hipLaunchKernelGGL(copy4, dim3(grid_copy), dim3(256), 0, s, (const f4*)x, (f4*)y, n / 4);
