@@ -63,12 +63,14 @@ struct Bucket {
   bool ready_timed = false;      // ev_ready recorded
 };
 
-// Timing events ride on the chain's own kernels (hipExtLaunchKernel's start / stop,
+// End marks ride on the chain's own kernels (hipExtLaunchKernel's stop event,
 // written by the dispatch) instead of event packets of their own: a packet costs
-// ~4.7 µs of stream time on the exposed chain, an event carried by a launch ~2.4 µs
-// (scripts/micro/event_chain.hip, profiles/r5/r5a_event_chain.jsonl).  arm() hands
-// the events to the plan's next launch; settle() records whatever no launch took
-// (an empty plan, a grad-view bucket that needs no scaling) at that point instead.
+// ~4.7 µs of stream time on the exposed chain, a kernel-carried stop event ~2.4 µs,
+// a kernel-carried START event ~7.4 µs (scripts/micro/event_chain.hip,
+// profiles/r5/r5a_event_chain.jsonl, r5f_event_chain.jsonl) — so start marks stay
+// packets.  arm() hands the events to the plan's next launch; settle() records
+// whatever no launch took (an empty plan, a grad-view bucket that needs no scaling)
+// at that point instead.
 void arm(gs_plan* p, hipEvent_t start, hipEvent_t stop) {
   p->once_start = start;
   p->once_stop = stop;
@@ -271,16 +273,19 @@ int launch_bucket(gs_bucketer* b, int bi) {
     hipEvent_t end_ev = chain_end ? (timed ? bk.ev_u1 : b->ev_done) : (timed ? bk.ev_u1 : nullptr);
     b->done_on_chain = chain_end;
     if (chain_end) b->done_ev = end_ev;
-    // pack: ext start / stop = pk0 / t0 (the pack or the grad-view scaling, whichever runs)
+    // pack: pk0 an event packet before it (a kernel-carried START event costs more
+    // stream time than a packet: 7.4 against 4.6 µs, profiles/r5/r5f_event_chain.jsonl),
+    // t0 the kernel's own stop event (the pack or the grad-view scaling, whichever runs)
     if (timed) {
-      arm(bk.plan, bk.ev_pk0, bk.ev_t0);
-      arm(bk.flat, bk.ev_pk0, bk.ev_t0);
+      HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
+      arm(bk.plan, nullptr, bk.ev_t0);
+      arm(bk.flat, nullptr, bk.ev_t0);
     }
     GS_TRY_RET(pack_raw(b, bk, cs));
     if (timed) {
-      // the launch consumed the events of the plan it ran on; the other plan's are dropped,
-      // and any left unconsumed on both (no kernel ran) are recorded here
-      const bool taken = bk.plan->once_start == nullptr || bk.flat->once_start == nullptr;
+      // the launch consumed the event of the plan it ran on; the other plan's is dropped,
+      // and one left unconsumed on both (no kernel ran) is recorded here
+      const bool taken = bk.plan->once_stop == nullptr || bk.flat->once_stop == nullptr;
       if (taken) {
         arm(bk.plan, nullptr, nullptr);
         arm(bk.flat, nullptr, nullptr);
@@ -292,9 +297,11 @@ int launch_bucket(gs_bucketer* b, int bi) {
     GS_TRY_RET(debug_sum(b, bk, 0, cs));
     GS_TRY_RET(launch_collective(b, bk, cs));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
-    // unpack: ext start / stop = t1 / (u1 or the done mark); the collective lies between t0 and t1
+    // unpack: t1 a packet before it, its stop = u1 or the done mark; the collective lies
+    // between t0 and t1
     if (b->do_unpack() || b->found_inf) {
-      GS_TRY_RET(unpack_one(b, bk, cs, 0, timed ? bk.ev_t1 : nullptr, end_ev));
+      if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
+      GS_TRY_RET(unpack_one(b, bk, cs, 0, nullptr, end_ev));
     } else if (timed) {
       HIPB_RET(hipEventRecord(bk.ev_t1, cs));
       HIPB_RET(hipEventRecord(bk.ev_u1, cs));

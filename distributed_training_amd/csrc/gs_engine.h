@@ -1057,42 +1057,51 @@ struct AdamOp {
 // last step, so the result is bit-identical to gs_sqnorm's), then exactly
 // clip_coef_kernel's arithmetic.  Workgroup 0 publishes [Σg², coef, norm].
 __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float* gscale) {
-  float sq;
-  if (c.groups > 0) {
-    // lane l: partials l, l + 64, ... in order (<= GS_RED_PARTIALS), then the tree;
-    // for <= 64 group sums exactly the fused combine's last step.  All loads are
-    // issued before the first add (one memory round trip per workgroup, not one per
-    // partial: a serial loop here cost the update 1.4 µs, profiles/r5/r5c_rows.jsonl);
-    // an absent partial adds +0 (the partials are sums of squares: never -0)
-    constexpr int kPer = GS_RED_PARTIALS / 64;
-    const int l = static_cast<int>(threadIdx.x & 63);
-    float v[kPer];
+  // wave 0 forms the coefficient, the workgroup reads it from LDS: one wave per
+  // workgroup reads the partial sums (every wave of every workgroup re-reading the
+  // same lines of L2 was the fold's cost).  Called uniformly by the whole workgroup.
+  __shared__ float s_coef;
+  if (threadIdx.x < 64) {
+    float sq;
+    if (c.groups > 0) {
+      // lane l: partials l, l + 64, ... in order (<= GS_RED_PARTIALS), then the tree;
+      // for <= 64 group sums exactly the fused combine's last step.  All loads are
+      // issued before the first add (one memory round trip, not one per partial);
+      // an absent partial adds +0 (the partials are sums of squares: never -0)
+      constexpr int kPer = GS_RED_PARTIALS / 64;
+      const int l = static_cast<int>(threadIdx.x);
+      float v[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int j = l + 64 * k;
-      v[k] = j < c.groups ? c.sq[j * c.stride] : 0.f;
+      for (int k = 0; k < kPer; ++k) {
+        const int j = l + 64 * k;
+        v[k] = j < c.groups ? c.sq[j * c.stride] : 0.f;
+      }
+      float x = 0.f;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) x = x + v[k];
+      sq = wave_sum(0.f + x);
+    } else {
+      sq = c.sq[0];
     }
-    float x = 0.f;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) x = x + v[k];
-    sq = wave_sum(0.f + x);
-  } else {
-    sq = c.sq[0];
+    const float s = gscale ? *gscale : 1.f;
+    if (gscale) sq = sq * (s * s);                    // the norm of the unscaled grads
+    sq = sq * c.sq_mul;
+    const float nrm = sqrtf(sq);
+    float coef = c.max_norm / (nrm + c.eps);
+    coef = coef < 1.f ? coef : 1.f;
+    if (gscale) coef = coef * s;
+    coef = coef * c.coef_mul;
+    if (threadIdx.x == 0) {
+      s_coef = coef;
+      if (c.out && blockIdx.x == 0) {
+        c.out[0] = sq;
+        c.out[1] = coef;
+        c.out[2] = nrm;
+      }
+    }
   }
-  const float s = gscale ? *gscale : 1.f;
-  if (gscale) sq = sq * (s * s);                    // the norm of the unscaled grads
-  sq = sq * c.sq_mul;
-  const float nrm = sqrtf(sq);
-  float coef = c.max_norm / (nrm + c.eps);
-  coef = coef < 1.f ? coef : 1.f;
-  if (gscale) coef = coef * s;
-  coef = coef * c.coef_mul;
-  if (c.out && blockIdx.x == 0 && threadIdx.x == 0) {
-    c.out[0] = sq;
-    c.out[1] = coef;
-    c.out[2] = nrm;
-  }
-  return coef;
+  __syncthreads();
+  return s_coef;
 }
 template <class Op>
 __device__ __forceinline__ void load_grad_multiplier(Op& op) {
@@ -1151,8 +1160,14 @@ struct DeviceGuard {
 // sums, which stay in the plan for the next clipped update (p->red_groups);
 // groups_only = 2 (raw, gs_sqnorm_partial_out on a small plan): a balanced grid of
 // <= GS_RED_PARTIALS workgroups, each writing its partial to red_out
-constexpr int kRawG = 8;  // chunks per group of the raw form: one group per workgroup
-constexpr int64_t kRawChunksMax = static_cast<int64_t>(kRawG) * GS_RED_PARTIALS;  // plans it serves
+// the raw form: groups of GS_G_RED chunks, at most kRawWorkgroups workgroups (= partials,
+// <= GS_RED_PARTIALS), each the same number of groups; plans of up to 4 Ki chunks
+#ifndef GS_RAW_WORKGROUPS
+#define GS_RAW_WORKGROUPS 512
+#endif
+constexpr int kRawWorkgroups = GS_RAW_WORKGROUPS;
+static_assert(kRawWorkgroups <= GS_RED_PARTIALS, "raw partials fit the caller's buffer");
+constexpr int64_t kRawChunksMax = 4096;
 template <class Op>
 int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumulate = 0,
            int groups_only = 0) {
@@ -1201,7 +1216,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
     if (raw) {
       // every workgroup the same number of groups (grid-stride over a balanced grid)
-      const int64_t per = (groups + GS_RED_PARTIALS - 1) / GS_RED_PARTIALS;
+      const int64_t per = (groups + kRawWorkgroups - 1) / kRawWorkgroups;
       grid = static_cast<int>(std::max<int64_t>(1, (groups + per - 1) / per));
     }
     PlanArgs a = p->args();

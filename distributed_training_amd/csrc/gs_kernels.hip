@@ -310,15 +310,6 @@ int hip_scale(gs_plan* p, int slot, int dt, float s, int mode, void* stream) {
 
 template <bool NT>
 static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
-  if (groups_only == 2) {
-    // raw partials of a small plan: groups of 8 chunks, one per workgroup (<= 512 of them)
-    GS_DISPATCH_FLOAT(dt, DT, {
-      SqnormOp<kUnit, DT, NT, kRawG> op;
-      op.slot = slot;
-      return launch(p, op, stream, sq, acc, groups_only);
-    });
-    return GS_OK;
-  }
   GS_DISPATCH_FLOAT(dt, DT, {
     SqnormOp<kUnit, DT, NT> op;
     op.slot = slot;
@@ -359,8 +350,8 @@ float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream) {
   DeviceGuard g(p->device);
   // caller memory on a small plan (<= 4 Ki chunks: a ZeRO shard at N = 8): one partial per
-  // workgroup, each streaming one group of 8 chunks with all its loads in flight at once,
-  // no counters and no combine — the kernel ends with its last store
+  // workgroup of a balanced grid, no counters and no combine — the kernel ends with its
+  // last store (groups of 8 chunks, one per workgroup, measured 0.7 µs slower: r5f)
   if (groups_out && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
       static_cast<int64_t>(p->chunks.size()) <= kRawChunksMax) {
     GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 2, stream));

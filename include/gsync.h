@@ -234,21 +234,21 @@ int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float 
  * groups_out (device memory of the plan's kind) must hold GS_RED_PARTIALS
  * floats; *n_groups (host) receives how many are valid, 1..GS_RED_PARTIALS.
  * A plan of at most 2 Ki chunk groups (a ZeRO shard at N = 8: 3.2 M elements)
- * writes one partial per workgroup of a balanced grid of <= GS_RED_PARTIALS
- * workgroups — no arrival counters, no in-kernel combine, nothing after the
+ * writes one partial per workgroup of a balanced grid (<= 512 workgroups) —
+ * no arrival counters, no in-kernel combine, nothing after the
  * streaming but one store per workgroup; a larger plan writes the fused
  * reduction's <= 64 group sums (gs_sqnorm_partial's kernel); 1 = a finished Σ
  * (host plans, a reduction without the in-kernel combine).  A sharded
  * optimizer SUM-all-reduces the whole GS_RED_PARTIALS-float buffer across its
  * ranks (slots past n stay zero and fold as zero, so the message never depends
- * on a rank's own grid) and hands it to gs_plan_set_clip_groups: the global ‖g‖
+ * on a rank's own grid; 8 KiB) and hands it to gs_plan_set_clip_groups: the global ‖g‖
  * of every shard with no combine launch and no scalar coefficient launch on the
  * step's exposed end.
  * replaces: DeepSpeed stage_1_and_2 get_grad_norm_direct (per-rank Σg² of the
  *           partition, all_reduce of the scalar, U) for gradient_clipping
  *           (R:resnet/deepspeed/deepspeed_train.py:195) */
 #define GS_RED_GROUPS 64
-#define GS_RED_PARTIALS 512
+#define GS_RED_PARTIALS 2048
 int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, int32_t* n_groups,
                           void* stream);
 /* gs_plan_set_clip with ‖g‖² = the fold of n_groups (<= GS_RED_PARTIALS)
@@ -386,15 +386,18 @@ int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
 /* per-bucket timeline of the last iteration (HIP events; -1 where untimed:
  * host buckets, external collectives, hipGraph capture), ms:
- *   out[0] queue      bucket ready on the producer -> comm stream starts it
- *   out[1] pack       out[2] collective       out[3] unpack (+ fused checks)
- *   out[4] ready -> every bucket finished (the finalize event): for the last
- *          bucket this is the exposed end-of-backward tail */
+ *   out[0] queue      bucket ready on the producer -> its pack kernel starts
+ *   out[1] pack       out[2] collective (pack end -> unpack start)
+ *   out[3] unpack (+ fused checks)
+ *   out[4] ready -> every bucket finished: for the last bucket this is the
+ *          exposed end-of-backward tail */
 int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out /* [5] */);
-/* which timing events the bucketer records (each is a packet on its stream;
- * on the exposed chain they cost ~10 µs apiece): 0 none; 1 (default) the last
- * bucket's ready event + the finalize event — out[4] of the last bucket, the
- * tail; 2 every bucket's full timeline (and gs_bucketer_last_comm_ms) */
+/* which timing marks the bucketer takes: 0 none; 1 (default) the last bucket's
+ * ready event + the "every chain done" mark — out[4] of the last bucket, the
+ * tail; 2 every bucket's full timeline (and gs_bucketer_last_comm_ms).  The
+ * ready mark is an event packet (~4.7 µs of stream time on the exposed chain);
+ * every other mark rides on the chain's own kernels (hipExtLaunchKernel start /
+ * stop events, ~2.4 µs) and becomes a packet only where no kernel runs */
 int gs_bucketer_set_timeline(gs_bucketer* b, int level);
 /* the HIP stream bucket `bucket`'s chain (pack -> collective -> unpack) was
  * enqueued on in this backward (the comm stream, or the producer stream for the

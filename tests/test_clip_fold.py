@@ -216,7 +216,7 @@ def test_clip_groups_fold_host(n):
     want = np.float32(-0.1) * np.float32(np.float32(1.0) * coef)  # fmaf(-lr, g·coef, 0)
     assert torch.equal(p, torch.full((16,), float(want)))
     with pytest.raises(D._lib.GsyncError, match="n_groups"):
-        plan.set_clip_groups(1.0, 1e-6, torch.zeros(1024), D._lib.GS_RED_PARTIALS + 1)
+        plan.set_clip_groups(1.0, 1e-6, torch.zeros(D._lib.GS_RED_PARTIALS + 1), D._lib.GS_RED_PARTIALS + 1)
     with pytest.raises(ValueError, match="partial sums"):
         plan.set_clip_groups(1.0, 1e-6, groups[:8], 9)
 
