@@ -285,9 +285,10 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     write), every launch and the collective timed together (HIP events on the
     stream they run on), over the engine's RCCL communicator (one rank here):
 
-    * ``clip_path_zero_n8``: Σg² group sums of the shard (gs_sqnorm_partial_out)
-      -> ONE SUM all-reduce of those <= 64 floats -> the AdamW update folding them
-      (gs_plan_set_clip_groups) — round 4's path;
+    * ``clip_path_zero_n8``: Σg² partial sums of the shard (gs_sqnorm_partial_out:
+      one per workgroup of a <= 1024-workgroup grid at this size, 780 floats)
+      -> ONE SUM all-reduce of them -> the AdamW update folding them
+      (gs_plan_set_clip_groups) — the round-4/5 path;
     * ``clip_path_zero_n8_scalar``: round 3's form — Σg² with its in-kernel
       combine -> SUM all-reduce of the scalar -> the update (gs_plan_set_clip).
 
@@ -315,10 +316,11 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     def adam():
         plan.adam(torch.bfloat16, 1e-3, 0.8, 0.999, 1e-8, 3e-7, True, False, -1e-3, 0.5, lowp_dtype=torch.bfloat16)
 
-    def folded():  # as zero.py: the whole partial-sum buffer travels and is folded
-        plan.sqnorm_partial_out(1, torch.bfloat16, groups)
-        comm.all_reduce(groups, stream=stream)
-        plan.set_clip_groups(1.0, 1e-6, groups, groups.numel(), out=out)
+    def folded():  # as zero.py
+        n = plan.sqnorm_partial_out(1, torch.bfloat16, groups)
+        nf = n if n > L.GS_RED_GROUPS else L.GS_RED_GROUPS
+        comm.all_reduce(groups[:nf], stream=stream)
+        plan.set_clip_groups(1.0, 1e-6, groups, nf, out=out)
         adam()
 
     def scalar():
@@ -373,7 +375,7 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
                       "host_paced_ms": host_ms,
                       "timing": ("HIP events around the call, the stream pre-loaded by a spin kernel (the launches "
                                  "queued ahead, as behind backward)" if spin else "HIP events around the call"),
-                      "launches": ("sqnorm_partial_out + all_reduce(<=64 floats) + clipped AdamW"
+                      "launches": ("sqnorm_partial_out + all_reduce(partials) + clipped AdamW"
                                    if name == "clip_path_zero_n8" else
                                    "sqnorm (in-kernel combine) + all_reduce(scalar) + clipped AdamW")}
     plan.set_clip(None)

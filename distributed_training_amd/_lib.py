@@ -32,7 +32,7 @@ GS_SUM, GS_PROD, GS_MAX, GS_MIN, GS_AVG = 0, 1, 2, 3, 4
 GS_SCALE_NONE, GS_SCALE_MUL, GS_SCALE_DIV = 0, 1, 2
 GS_PLAN_SLOTS = 5
 GS_RED_GROUPS = 64  # the fused reduction's group sums (one per lane of the folding wave)
-GS_RED_PARTIALS = 2048  # gs_sqnorm_partial_out: the caller's buffer, at most this many partial sums
+GS_RED_PARTIALS = 1024  # gs_sqnorm_partial_out: the caller's buffer, at most this many partial sums
 GS_BKT_AUTO_COLLECTIVE = 1
 GS_BKT_GRAD_VIEW = 2
 GS_BKT_NO_SCALE = 4

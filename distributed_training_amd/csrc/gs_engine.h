@@ -1163,7 +1163,7 @@ struct DeviceGuard {
 // the raw form: groups of GS_G_RED chunks, at most kRawWorkgroups workgroups (= partials,
 // <= GS_RED_PARTIALS), each the same number of groups; plans of up to 4 Ki chunks
 #ifndef GS_RAW_WORKGROUPS
-#define GS_RAW_WORKGROUPS 512
+#define GS_RAW_WORKGROUPS 1024  // 256 / 512 / 1024 / 2048: 7.1 / 4.7-5.1 / 4.4-4.5 / 4.3-4.4 µs (r5g)
 #endif
 constexpr int kRawWorkgroups = GS_RAW_WORKGROUPS;
 static_assert(kRawWorkgroups <= GS_RED_PARTIALS, "raw partials fit the caller's buffer");

@@ -393,7 +393,7 @@ int gs_plan_set_clip_groups(gs_plan* p, const float* groups_dev, int32_t n_group
     return GS_OK;
   }
   GS_CHECK_ARG(groups_dev != nullptr, "gs_plan_set_clip_groups: NULL group sums");
-  GS_CHECK_ARG(n_groups >= 1 && n_groups <= GS_RED_PARTIALS, "gs_plan_set_clip_groups: n_groups out of 1..512");
+  GS_CHECK_ARG(n_groups >= 1 && n_groups <= GS_RED_PARTIALS, "gs_plan_set_clip_groups: n_groups out of 1..GS_RED_PARTIALS");
   GS_CHECK_ARG(eps >= 0.f, "gs_plan_set_clip_groups: eps < 0");
   p->clip_on = true;
   p->clip_own = false;

@@ -12,8 +12,8 @@ one bucket for ResNet-18/50):
 backward: hooks pack each bucket and RCCL reduce-scatters it (stage 2) or
           all-reduces it (stage 1) on libgsync's stream, under backward;
 step:     (fp16) non-finite check of the shard + MAX all-reduce of the flag,
-          (clip) Σg² group sums of the shard + one SUM all-reduce of those
-          <= 64 floats, folded into the update (no combine / coefficient
+          (clip) Σg² partial sums of the shard + one SUM all-reduce of
+          them (<= 1 Ki floats), folded into the update (no combine / coefficient
           launch); ONE fused Adam/SGD launch over all shards
           that also writes the low-precision params into this rank's slice
           of the param flat buffer; in-place all-gather of each bucket.
@@ -459,19 +459,20 @@ class ZeroDataParallel:
                 self.plan.set_clip(self.clip, 1e-6, None, inv_scale * inv_scale, inv_scale, out=s[4:7])
             else:
                 # this shard's Σg² partial sums (a small shard, e.g. ResNet-50 at N=8: one per
-                # workgroup of a <= 512-workgroup grid, no in-kernel combine) SUM-all-reduced
-                # over the ranks (one 2 KiB message, identical bits everywhere), folded by
-                # every update workgroup: Σg² kernel -> collective -> update, nothing in
-                # between (DeepSpeed: per-rank Σ, scalar all_reduce, coefficient, U).
-                # The whole buffer travels and is folded: the slots past this rank's count
-                # stay zero and add nothing (clip_multiplier folds absent partials as 0.f,
-                # so the bits do not depend on n), and the message length never depends on
-                # a rank's own grid
+                # workgroup of a <= 1024-workgroup grid, no in-kernel combine) SUM-all-reduced
+                # over the ranks (one message, identical bits everywhere), folded by every
+                # update workgroup: Σg² kernel -> collective -> update, nothing in between
+                # (DeepSpeed: per-rank Σ, scalar all_reduce, coefficient, U).  The message
+                # length never depends on a rank's own reduction settings: slots
+                # past a rank's count stay zero and add nothing (clip_multiplier folds absent
+                # partials as 0.f, so the bits do not depend on n)
                 gr = self._red_groups
-                self.plan.sqnorm_partial_out(1, self.dtype, gr)
-                self._allreduce_scalar(gr, "sum")
-                self.plan.set_clip_groups(self.clip, 1e-6, gr, gr.numel(), inv_scale * inv_scale, inv_scale,
-                                          out=s[4:7])
+                n = self.plan.sqnorm_partial_out(1, self.dtype, gr)
+                # raw partials (n > 64): n follows from the shard size alone, the same on
+                # every rank; the <= 64 group sums of the grouped form: all 64 slots travel
+                nf = n if n > L.GS_RED_GROUPS else L.GS_RED_GROUPS
+                self._allreduce_scalar(gr[:nf], "sum")
+                self.plan.set_clip_groups(self.clip, 1e-6, gr, nf, inv_scale * inv_scale, inv_scale, out=s[4:7])
         elif self.clip > 0:
             self.plan.set_clip(None)
             sq = s[1:2]

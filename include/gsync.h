@@ -234,21 +234,23 @@ int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float 
  * groups_out (device memory of the plan's kind) must hold GS_RED_PARTIALS
  * floats; *n_groups (host) receives how many are valid, 1..GS_RED_PARTIALS.
  * A plan of at most 2 Ki chunk groups (a ZeRO shard at N = 8: 3.2 M elements)
- * writes one partial per workgroup of a balanced grid (<= 512 workgroups) —
+ * writes one partial per workgroup of a balanced grid (<= 1024 workgroups) —
  * no arrival counters, no in-kernel combine, nothing after the
  * streaming but one store per workgroup; a larger plan writes the fused
  * reduction's <= 64 group sums (gs_sqnorm_partial's kernel); 1 = a finished Σ
  * (host plans, a reduction without the in-kernel combine).  A sharded
  * optimizer SUM-all-reduces the whole GS_RED_PARTIALS-float buffer across its
- * ranks (slots past n stay zero and fold as zero, so the message never depends
- * on a rank's own grid; 8 KiB) and hands it to gs_plan_set_clip_groups: the global ‖g‖
+ * ranks — the first max(n, GS_RED_GROUPS) floats: n is a function of the plan's
+ * size alone where it exceeds GS_RED_GROUPS (the raw form's grid is a build
+ * constant), so every rank sends the same length; slots past a rank's n stay
+ * zero and fold as zero — and hands them to gs_plan_set_clip_groups: the global ‖g‖
  * of every shard with no combine launch and no scalar coefficient launch on the
  * step's exposed end.
  * replaces: DeepSpeed stage_1_and_2 get_grad_norm_direct (per-rank Σg² of the
  *           partition, all_reduce of the scalar, U) for gradient_clipping
  *           (R:resnet/deepspeed/deepspeed_train.py:195) */
 #define GS_RED_GROUPS 64
-#define GS_RED_PARTIALS 2048
+#define GS_RED_PARTIALS 1024
 int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, int32_t* n_groups,
                           void* stream);
 /* gs_plan_set_clip with ‖g‖² = the fold of n_groups (<= GS_RED_PARTIALS)

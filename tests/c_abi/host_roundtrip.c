@@ -87,7 +87,7 @@ int main(void) {
       printf("FAIL clip groups %f %f %f\n", out[0], out[2], p0[0]);
       return 1;
     }
-    if (gs_plan_set_clip_groups(s0, grp0, GS_RED_GROUPS + 1, 1.f, 1e-6f, 1.f, 1.f, out) != GS_EINVAL) {
+    if (gs_plan_set_clip_groups(s0, grp0, GS_RED_PARTIALS + 1, 1.f, 1e-6f, 1.f, 1.f, out) != GS_EINVAL) {
       printf("FAIL clip groups range\n");
       return 1;
     }
