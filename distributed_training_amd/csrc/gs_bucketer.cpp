@@ -113,7 +113,7 @@ struct gs_bucketer {
   // queue / pack / collective / unpack.  Each timing event is a packet on the
   // stream; at level 2 they stretch the exposed chain by ~10 µs apiece.
   int timeline = 1;
-  hipEvent_t ev_comm = nullptr;     // comm stream's earlier buckets, joined before a producer-side tail
+  hipEvent_t ev_comm = nullptr;     // comm stream's earlier buckets, joined before a producer-side tail's collective
   bool done_timed = false;
   hipEvent_t done_ev = nullptr;     // this iteration's "every chain done" mark: ev_done, or the stop
                                     // event of the producer-side tail's last kernel (done_on_chain)
@@ -240,8 +240,9 @@ int launch_bucket(gs_bucketer* b, int bi) {
     // The last bucket's chain is the exposed end-of-backward tail: nothing is
     // left to overlap it with, so it runs on the producer stream itself — no
     // cross-stream hop to start it (its "queue") and none back at finalize.
-    // The producer first joins the comm stream's earlier buckets, so the
-    // communicator's collectives stay in issue order on the GPU.
+    // The producer joins the comm stream's earlier buckets after its pack, right
+    // before its collective, so the communicator's collectives stay in issue
+    // order on the GPU while the pack overlaps the previous bucket's chain.
     const bool last = bi == static_cast<int>(b->buckets.size()) - 1;
     const bool on_producer = last;
     hipStream_t ps = static_cast<hipStream_t>(b->producer);
@@ -257,10 +258,7 @@ int launch_bucket(gs_bucketer* b, int bi) {
       HIPB_RET(hipEventRecord(bk.ev_sync, ps));
     }
     if (on_producer) {
-      if (bi > 0) {
-        HIPB_RET(hipEventRecord(b->ev_comm, comm_stream(b->comm)));
-        HIPB_RET(hipStreamWaitEvent(ps, b->ev_comm, 0));
-      }
+      if (bi > 0) HIPB_RET(hipEventRecord(b->ev_comm, comm_stream(b->comm)));
       b->tail_ran_on_producer = true;
     } else {
       HIPB_RET(hipStreamWaitEvent(cs, bk.ready_timed ? bk.ev_ready : bk.ev_sync, 0));
@@ -295,6 +293,7 @@ int launch_bucket(gs_bucketer* b, int bi) {
       }
     }
     GS_TRY_RET(debug_sum(b, bk, 0, cs));
+    if (on_producer && bi > 0) HIPB_RET(hipStreamWaitEvent(ps, b->ev_comm, 0));
     GS_TRY_RET(launch_collective(b, bk, cs));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
     // unpack: t1 a packet before it, its stop = u1 or the done mark; the collective lies
