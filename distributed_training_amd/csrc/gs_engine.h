@@ -153,20 +153,6 @@ inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
 #ifndef GS_RED_FUSE_GRID
 #define GS_RED_FUSE_GRID 2048  // workgroups of a fused reduction (r2z2 sweep: 2048 < 4096 < 8192)
 #endif
-// a capped reduction grid balanced so that every workgroup strides over the same
-// number of chunk groups (grid = ceil(groups / ceil(groups / cap))): the capped grid
-// otherwise leaves a last stride round to a few workgroups, latency-bound
-#ifndef GS_RED_BALANCED
-#define GS_RED_BALANCED 0
-#endif
-// a fused reduction of <= 32 workgroups per group (the 2 Ki fused grid, R = 64)
-// folds in ONE level: group leaders only arrive on the top counter and the last
-// one folds every partial itself (chunk_kernel), one hand-off fewer on the
-// critical path after the last workgroup; bit-identical to the two-level fold
-#ifndef GS_RED_ONE_LEVEL
-#define GS_RED_ONE_LEVEL 0
-#endif
-constexpr int kOneLevelPer = 32;  // partial slots per group (one half-wave)
 constexpr int kRedSyncWords = (2 * kRedMaxGroups + 1) * kRedSyncStride;
 constexpr int kRedFuseMaxGrid = 8192;  // above this a group's counter sees too many arrivals
 // chunks per workgroup iteration (chunk-map engine), per op: profiles/r2*_kernels_*.jsonl,
@@ -377,21 +363,6 @@ __device__ __forceinline__ float wave_reduce(float v) {
   v = dpp_op<0x142, 0xA, MAX>(v, id);  // row_bcast:15 into rows 1, 3
   v = dpp_op<0x143, 0xC, MAX>(v, id);  // row_bcast:31 into rows 2, 3
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-// The same tree stopped after row_bcast:15: lane 31 holds the fold of lanes 0-31
-// and lane 63 that of lanes 32-63, each bit-identical to wave_reduce of those 32
-// lanes with the other half at the identity (the skipped row_bcast:31 then adds
-// an exact 0 / max with -inf): two 32-value folds per pass
-template <bool MAX>
-__device__ __forceinline__ void wave_reduce_halves(float v, float& lo, float& hi) {
-  const float id = MAX ? -INFINITY : 0.f;
-  v = dpp_op<0xB1, 0xF, MAX>(v, id);
-  v = dpp_op<0x4E, 0xF, MAX>(v, id);
-  v = dpp_op<0x141, 0xF, MAX>(v, id);
-  v = dpp_op<0x140, 0xF, MAX>(v, id);
-  v = dpp_op<0x142, 0xA, MAX>(v, id);
-  lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
-  hi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 __device__ __forceinline__ float wave_sum(float v) { return wave_reduce<false>(v); }
 __device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v); }
@@ -669,72 +640,6 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
     const int n_groups = grid < R ? grid : R;
     uint32_t* top = &P.ticket[kRedMaxGroups * kStride];
     float* gsums = reinterpret_cast<float*>(P.ticket + (kRedMaxGroups + 1) * kStride);
-    if (GS_RED_ONE_LEVEL && !P.red_groups_only && R <= 64 && grid <= kOneLevelPer * R) {
-      // One level.  Workgroup b's partial goes to slot k * 32 + b / R (group k's
-      // partials contiguous), it drains and arrives on group k's counter; the
-      // group's last arriver re-arms it and arrives on the top counter; the last
-      // group's leader loads all partials (wave w, pass j: groups 16w + 2j and
-      // + 1, one per half-wave, coalesced), folds each half-wave with the
-      // two-level form's DPP tree and its block_reduce's three trailing
-      // identities, then folds the group sums in group order as it does.
-      if (threadIdx.x == 0) {
-        const uint32_t ng = static_cast<uint32_t>((grid - 1 - k) / R + 1);
-        __hip_atomic_store(&op.partials[k * kOneLevelPer + static_cast<int>(blockIdx.x) / R], r, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(&P.ticket[k * kStride], 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-        int role = 0;
-        if (tk == ng - 1) {
-          __hip_atomic_store(&P.ticket[k * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t t2 = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          role = t2 == static_cast<uint32_t>(n_groups) - 1;
-        }
-        s_role = role;
-      }
-      __syncthreads();
-      if (!s_role) return;  // uniform within the workgroup
-      __shared__ float s_g[64];
-      const int w = static_cast<int>(threadIdx.x) >> 6, l = static_cast<int>(threadIdx.x) & 63;
-      float y[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int g = 16 * w + 2 * j + (l >> 5), t = l & 31;
-        const int ngg = g < n_groups ? (grid - 1 - g) / R + 1 : 0;
-        y[j] = 0.f;
-        if (t < ngg) {
-          const float x = __hip_atomic_load(&op.partials[g * kOneLevelPer + t], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-          y[j] = MAX ? fmaxf(0.f, x) : 0.f + x;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float a, b;
-        wave_reduce_halves<MAX>(y[j], a, b);
-#pragma unroll
-        for (int u = 1; u < kBlock / 64; ++u) {  // block_reduce's other (all-zero) waves
-          a = MAX ? fmaxf(a, 0.f) : a + 0.f;
-          b = MAX ? fmaxf(b, 0.f) : b + 0.f;
-        }
-        if (l == 0) {
-          s_g[16 * w + 2 * j] = a;
-          s_g[16 * w + 2 * j + 1] = b;
-        }
-      }
-      __syncthreads();
-      if (w != 0) return;
-      float t = 0.f;
-      if (l < n_groups) t = MAX ? fmaxf(t, s_g[l]) : t + s_g[l];
-      const float tot = MAX ? wave_max(t) : wave_sum(t);
-      if (l == 0) {
-        float* out = P.red_out;
-        if (MAX) out[0] = P.red_acc ? fmaxf(out[0], tot) : tot;
-        else out[0] = P.red_acc ? out[0] + tot : tot;
-        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
     if (threadIdx.x == 0) {
       const uint32_t ng = static_cast<uint32_t>((grid - 1 - k) / R + 1);
       __hip_atomic_store(&op.partials[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1309,10 +1214,6 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
     // any fused reduction overwrites the group sums a gs_sqnorm_partial left
     if (fused && !groups_only) p->red_valid = false;
     grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(groups, cap)));
-    if (GS_RED_BALANCED && red && !raw && groups > grid) {
-      const int64_t per = (groups + grid - 1) / grid;
-      grid = static_cast<int>((groups + per - 1) / per);
-    }
     if (raw) {
       // every workgroup the same number of groups (grid-stride over a balanced grid)
       const int64_t per = (groups + kRawWorkgroups - 1) / kRawWorkgroups;

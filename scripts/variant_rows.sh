@@ -3,15 +3,18 @@
 # _gshook.so) against the default, interleaved over two rounds: bench.py with
 # the kernel rates (configs[3]'s N=8-shard clip path included), the exposed
 # tail's split; one JSON line per run into <out>/rows.jsonl.
-#   VARIANTS="a b c" scripts/variant_rows.sh <out dir>
+#   VARIANTS="a b c" [ENV_c="VAR=VALUE"] scripts/variant_rows.sh <out dir>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$1; mkdir -p $OUT
 export TMPDIR=/tmp
 for r in 1 2; do
   for v in default $VARIANTS; do
-    if [ $v = default ]; then unset GSYNC_LIB; else export GSYNC_LIB=$PWD/distributed_training_amd/lib/variants/$v/libgsync.so; fi
-    timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --zero-leg 0 --colossal-leg 0 --cpu-baseline 0 --parity 0 > $OUT/b_${v}_$r.json 2> $OUT/b_${v}_$r.err || { tail -20 $OUT/b_${v}_$r.err; exit 1; }
+    # a variant is a library build (lib/variants/<name>/) or, when ENV_<name> is set,
+    # the default library under that VAR=VALUE environment setting
+    envv=$(eval echo "\${ENV_$v:-}")
+    if [ $v = default ] || [ -n "$envv" ]; then unset GSYNC_LIB; else export GSYNC_LIB=$PWD/distributed_training_amd/lib/variants/$v/libgsync.so; fi
+    env $envv timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --zero-leg 0 --colossal-leg 0 --cpu-baseline 0 --parity 0 > $OUT/b_${v}_$r.json 2> $OUT/b_${v}_$r.err || { tail -20 $OUT/b_${v}_$r.err; exit 1; }
     python3 - "$OUT/b_${v}_$r.json" "$v" "$r" >> $OUT/rows.jsonl <<'PY'
 import json, sys
 d = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
