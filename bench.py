@@ -286,8 +286,9 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     stream they run on), over the engine's RCCL communicator (one rank here):
 
     * ``clip_path_zero_n8``: Σg² partial sums of the shard (gs_sqnorm_partial_out:
-      one per workgroup of a <= 1024-workgroup grid at this size, 780 floats)
-      -> ONE SUM all-reduce of them -> the AdamW update folding them
+      one per workgroup of a <= 1024-workgroup grid at this size, 780 floats, in
+      a 1 Ki-float buffer) -> ONE SUM all-reduce of the buffer -> the AdamW update
+      folding it
       (gs_plan_set_clip_groups) — the round-4/5 path;
     * ``clip_path_zero_n8_scalar``: round 3's form — Σg² with its in-kernel
       combine -> SUM all-reduce of the scalar -> the update (gs_plan_set_clip).
@@ -316,11 +317,10 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     def adam():
         plan.adam(torch.bfloat16, 1e-3, 0.8, 0.999, 1e-8, 3e-7, True, False, -1e-3, 0.5, lowp_dtype=torch.bfloat16)
 
-    def folded():  # as zero.py
-        n = plan.sqnorm_partial_out(1, torch.bfloat16, groups)
-        nf = n if n > L.GS_RED_GROUPS else L.GS_RED_GROUPS
-        comm.all_reduce(groups[:nf], stream=stream)
-        plan.set_clip_groups(1.0, 1e-6, groups, nf, out=out)
+    def folded():  # as zero.py: the whole partial-sum buffer travels and is folded
+        plan.sqnorm_partial_out(1, torch.bfloat16, groups)
+        comm.all_reduce(groups, stream=stream)
+        plan.set_clip_groups(1.0, 1e-6, groups, groups.numel(), out=out)
         adam()
 
     def scalar():

@@ -60,6 +60,8 @@ struct Bucket {
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
   hipEvent_t ev_sync = nullptr;  // untimed ready event (a comm-stream chain waits on it)
   bool timed = false;            // pk0 / t0 / t1 / u1 recorded (level 2)
+  bool pk0_is_ready = false;     // the producer-side tail: its pack follows the ready mark on the same
+                                 // stream with nothing between, so ready doubles as pk0 (queue 0)
   bool ready_timed = false;      // ev_ready recorded
 };
 
@@ -276,8 +278,10 @@ int launch_bucket(gs_bucketer* b, int bi) {
     // pack: pk0 an event packet before it (a kernel-carried START event costs more
     // stream time than a packet: 7.4 against 4.6 µs, profiles/r5/r5f_event_chain.jsonl),
     // t0 the kernel's own stop event (the pack or the grad-view scaling, whichever runs)
+    // (the producer-side tail: no pk0 packet, ready is its pack's start)
+    bk.pk0_is_ready = timed && on_producer;
     if (timed) {
-      HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
+      if (!on_producer) HIPB_RET(hipEventRecord(bk.ev_pk0, cs));
       arm(bk.plan, nullptr, bk.ev_t0);
       arm(bk.flat, nullptr, bk.ev_t0);
     }
@@ -613,8 +617,9 @@ int gs_bucketer_last_timing(gs_bucketer* b, int bucket, float* out) {
   if (!b->hip() || !b->auto_coll()) return GS_OK;
   if (bk.timed && bk.ready_timed) {
     HIPB_RET(hipEventSynchronize(bk.ev_u1));
-    HIPB_RET(hipEventElapsedTime(&out[0], bk.ev_ready, bk.ev_pk0));
-    HIPB_RET(hipEventElapsedTime(&out[1], bk.ev_pk0, bk.ev_t0));
+    hipEvent_t pk0 = bk.pk0_is_ready ? bk.ev_ready : bk.ev_pk0;
+    HIPB_RET(hipEventElapsedTime(&out[0], bk.ev_ready, pk0));
+    HIPB_RET(hipEventElapsedTime(&out[1], pk0, bk.ev_t0));
     HIPB_RET(hipEventElapsedTime(&out[2], bk.ev_t0, bk.ev_t1));
     HIPB_RET(hipEventElapsedTime(&out[3], bk.ev_t1, bk.ev_u1));
   }

@@ -614,6 +614,10 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
       // raw (gs_sqnorm_partial_out on a small plan): the partial goes straight to the
       // caller's buffer, stream-ordered for its consumer; else to the combine's input
       if (threadIdx.x == 0) (P.red_raw ? P.red_out : op.partials)[blockIdx.x] = r;
+      // ... and workgroup 0 zeroes the buffer's slots past the grid: a sharded caller
+      // sums the whole buffer across ranks whose partial counts may differ
+      if (P.red_raw && blockIdx.x == 0)
+        for (int i = static_cast<int>(gridDim.x + threadIdx.x); i < GS_RED_PARTIALS; i += kBlock) P.red_out[i] = 0.f;
       return;
     }
     // In-kernel combine, two-level ticket.  Workgroup b belongs to group
@@ -640,6 +644,9 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
     const int n_groups = grid < R ? grid : R;
     uint32_t* top = &P.ticket[kRedMaxGroups * kStride];
     float* gsums = reinterpret_cast<float*>(P.ticket + (kRedMaxGroups + 1) * kStride);
+    // gs_sqnorm_partial_out: the caller's slots past the group count read 0 (as in the raw form)
+    if (P.red_groups_only && P.red_out && blockIdx.x == 0)
+      for (int i = n_groups + static_cast<int>(threadIdx.x); i < GS_RED_PARTIALS; i += kBlock) P.red_out[i] = 0.f;
     if (threadIdx.x == 0) {
       const uint32_t ng = static_cast<uint32_t>((grid - 1 - k) / R + 1);
       __hip_atomic_store(&op.partials[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -369,9 +369,11 @@ int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t*
   p->red_groups = 0;
   if (n_groups) *n_groups = 1;
   GS_TRY_RET(sqnorm_launch(p, slot, dt, hip_plan_red_scalar(p), 0, 0, stream));
-  if (groups_out)
+  if (groups_out) {  // the finished Σ in slot 0, the rest of the buffer 0
+    HIP_RET(hipMemsetAsync(groups_out, 0, GS_RED_PARTIALS * sizeof(float), static_cast<hipStream_t>(stream)));
     HIP_RET(hipMemcpyAsync(groups_out, hip_plan_red_scalar(p), sizeof(float), hipMemcpyDeviceToDevice,
                            static_cast<hipStream_t>(stream)));
+  }
   return GS_OK;
 }
 

@@ -365,6 +365,7 @@ int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, in
     p->red_groups = 0;
     GS_TRY_RET(host_sqnorm(p, slot, dtype, &p->h_red, 0));
     groups_out[0] = p->h_red;
+    std::fill(groups_out + 1, groups_out + GS_RED_PARTIALS, 0.f);
     *n_groups = 1;
     return GS_OK;
   }

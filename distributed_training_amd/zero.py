@@ -463,16 +463,16 @@ class ZeroDataParallel:
                 # over the ranks (one message, identical bits everywhere), folded by every
                 # update workgroup: Σg² kernel -> collective -> update, nothing in between
                 # (DeepSpeed: per-rank Σ, scalar all_reduce, coefficient, U).  The message
-                # length never depends on a rank's own reduction settings: slots
-                # past a rank's count stay zero and add nothing (clip_multiplier folds absent
-                # partials as 0.f, so the bits do not depend on n)
+                # length never depends on a rank's own chunk map or reduction settings
+                # (ADVICE r4): slots past a rank's count stay zero and add nothing
                 gr = self._red_groups
-                n = self.plan.sqnorm_partial_out(1, self.dtype, gr)
-                # raw partials (n > 64): n follows from the shard size alone, the same on
-                # every rank; the <= 64 group sums of the grouped form: all 64 slots travel
-                nf = n if n > L.GS_RED_GROUPS else L.GS_RED_GROUPS
-                self._allreduce_scalar(gr[:nf], "sum")
-                self.plan.set_clip_groups(self.clip, 1e-6, gr, nf, inv_scale * inv_scale, inv_scale, out=s[4:7])
+                self.plan.sqnorm_partial_out(1, self.dtype, gr)
+                # the whole buffer travels and is folded: a rank's partial count follows
+                # its shard's chunk map (tensor pieces split at shard edges differ from
+                # rank to rank), so no count-dependent length is safe to send
+                self._allreduce_scalar(gr, "sum")
+                self.plan.set_clip_groups(self.clip, 1e-6, gr, gr.numel(), inv_scale * inv_scale, inv_scale,
+                                          out=s[4:7])
         elif self.clip > 0:
             self.plan.set_clip(None)
             sq = s[1:2]

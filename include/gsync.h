@@ -232,18 +232,19 @@ int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float 
                      float coef_mul, float* out_dev);
 /* The partial sums of Σx² over the plan, written out for a sharded optimizer:
  * groups_out (device memory of the plan's kind) must hold GS_RED_PARTIALS
- * floats; *n_groups (host) receives how many are valid, 1..GS_RED_PARTIALS.
- * A plan of at most 2 Ki chunk groups (a ZeRO shard at N = 8: 3.2 M elements)
+ * floats; *n_groups (host) receives how many are valid, 1..GS_RED_PARTIALS,
+ * and the call sets the slots past them to 0.
+ * A plan of at most 4 Ki chunks (a ZeRO shard at N = 8: 3.2 M elements)
  * writes one partial per workgroup of a balanced grid (<= 1024 workgroups) —
  * no arrival counters, no in-kernel combine, nothing after the
  * streaming but one store per workgroup; a larger plan writes the fused
  * reduction's <= 64 group sums (gs_sqnorm_partial's kernel); 1 = a finished Σ
  * (host plans, a reduction without the in-kernel combine).  A sharded
  * optimizer SUM-all-reduces the whole GS_RED_PARTIALS-float buffer across its
- * ranks — the first max(n, GS_RED_GROUPS) floats: n is a function of the plan's
- * size alone where it exceeds GS_RED_GROUPS (the raw form's grid is a build
- * constant), so every rank sends the same length; slots past a rank's n stay
- * zero and fold as zero — and hands them to gs_plan_set_clip_groups: the global ‖g‖
+ * ranks (a rank's n follows its own chunk map, so only a fixed length is the
+ * same on every rank; the zero slots past a rank's n add nothing) and hands it
+ * to gs_plan_set_clip_groups
+ * (n_groups = GS_RED_PARTIALS): the global ‖g‖
  * of every shard with no combine launch and no scalar coefficient launch on the
  * step's exposed end.
  * replaces: DeepSpeed stage_1_and_2 get_grad_norm_direct (per-rank Σg² of the

@@ -69,7 +69,7 @@ int main(void) {
     void* gp1[1] = {g1};
     CHECK(gs_plan_set_ptrs(s0, 1, gp0, NULL));
     CHECK(gs_plan_set_ptrs(s1, 1, gp1, NULL));
-    float grp0[GS_RED_GROUPS], grp1[GS_RED_GROUPS];
+    float grp0[GS_RED_PARTIALS], grp1[GS_RED_PARTIALS];  /* the buffer the call requires */
     int32_t n0 = 0, n1 = 0;
     CHECK(gs_sqnorm_partial_out(s0, 1, GS_F32, grp0, &n0, NULL));
     CHECK(gs_sqnorm_partial_out(s1, 1, GS_F32, grp1, &n1, NULL));

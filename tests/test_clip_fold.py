@@ -222,15 +222,16 @@ def test_clip_groups_fold_host(n):
 
 
 def test_sqnorm_partial_out_host():
-    """Host plans: one group, the finished Σg² (what gs_sqnorm gives)."""
+    """Host plans: one group, the finished Σg² (what gs_sqnorm gives); the slots
+    past it are zeroed (a sharded caller all-reduces the whole buffer)."""
     xs = [torch.randn(n, generator=torch.Generator().manual_seed(n)) for n in (7, 1000, 33)]
     plan = D.multi_tensor.TensorListPlan([x.numel() for x in xs], torch.device("cpu"), task_units=0)
     plan.set_ptrs(1, xs)
-    gr = torch.zeros(D._lib.GS_RED_PARTIALS)
+    gr = torch.full((D._lib.GS_RED_PARTIALS,), 7.0)
     n = plan.sqnorm_partial_out(1, torch.float32, gr)
     ref = torch.zeros(1)
     plan.sqnorm(1, torch.float32, ref)
-    assert n == 1 and gr[0].item() == ref.item()
+    assert n == 1 and gr[0].item() == ref.item() and not gr[1:].any()
     with pytest.raises(ValueError, match="partial sums"):
         plan.sqnorm_partial_out(1, torch.float32, torch.zeros(64))
 
@@ -309,18 +310,18 @@ def test_clip_groups_fold_gpu_equals_host_and_sqnorm():
     xs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
     plan = D.multi_tensor.TensorListPlan(sizes, dev)
     plan.set_ptrs(1, xs)
-    gr = torch.zeros(D._lib.GS_RED_PARTIALS, device=dev)
+    gr = torch.full((D._lib.GS_RED_PARTIALS,), 7.0, device=dev)  # stale slots: zeroed by the call
     n = plan.sqnorm_partial_out(1, torch.float32, gr)
     ref = torch.zeros(1, device=dev)
     plan.sqnorm(1, torch.float32, ref)
     torch.cuda.synchronize()
-    assert n == 64
+    assert n == 64 and not gr[n:].any()
     assert float(np.float32(_dpp_wave_sum(gr.cpu().numpy()[:n]))) == ref.item()
     # the raw form: 3.2 M bf16 elements (ResNet-50 / 8), one partial per workgroup
     shard = (torch.randn(3194688, device=dev, generator=gen) * 1e-3).to(torch.bfloat16)
     small = D.multi_tensor.TensorListPlan([shard.numel()], dev)
     small.set_ptrs(1, [shard])
-    gr.zero_()
+    gr.fill_(7.0)
     n = small.sqnorm_partial_out(1, torch.bfloat16, gr)
     torch.cuda.synchronize()
     parts = gr.cpu().numpy()
