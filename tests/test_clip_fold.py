@@ -338,6 +338,48 @@ def test_clip_groups_fold_gpu_equals_host_and_sqnorm():
     assert out[0].item() == float(np.float32(_dpp_wave_sum(parts[:n])))
 
 
+@pytest.mark.gpu
+def test_sharded_partials_with_different_counts_gpu():
+    """ZeRO's world > 1 clip when two ranks' shards have different chunk maps (the
+    same element count split into different tensor pieces): their raw partial
+    counts differ, so the whole GS_RED_PARTIALS buffer travels and is folded.
+    Buffers start stale (the call zeroes the slots past its count); their sum (the
+    all-reduce) folded over all GS_RED_PARTIALS slots gives the exact Σg² of both
+    shards to fp32 rounding, bit-equal to the restated fold, on a second call too."""
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(13)
+    total = 3194688
+    a = (torch.randn(total, device=dev, generator=gen) * 1e-3).to(torch.bfloat16)
+    pieces = [999] * (total // 999) + [total % 999]  # 64-aligned: ~one chunk per piece
+    b_flat = (torch.randn(total, device=dev, generator=gen) * 1e-3).to(torch.bfloat16)
+    b = list(b_flat.split(pieces))
+    pa = D.multi_tensor.TensorListPlan([total], dev)
+    pa.set_ptrs(1, [a])
+    pb = D.multi_tensor.TensorListPlan(pieces, dev, align=64)
+    pb.set_ptrs(1, b)
+    exact = float((a.double() ** 2).sum() + (b_flat.double() ** 2).sum())
+    P = D._lib.GS_RED_PARTIALS
+    for _ in range(2):
+        ga = torch.full((P,), 5.0, device=dev)
+        gb = torch.full((P,), 3.0, device=dev)
+        na = pa.sqnorm_partial_out(1, torch.bfloat16, ga)
+        nb = pb.sqnorm_partial_out(1, torch.bfloat16, gb)
+        torch.cuda.synchronize()
+        assert na != nb and 64 < min(na, nb) and max(na, nb) <= P, (na, nb)
+        assert not ga[na:].any() and not gb[nb:].any()
+        tot = ga + gb  # the SUM all-reduce of two ranks
+        p1, g1, b1 = (torch.zeros(8, device=dev), torch.ones(8, device=dev), torch.zeros(8, device=dev))
+        up = D.multi_tensor.TensorListPlan([8], dev)
+        for k, t in enumerate((p1, g1, b1)):
+            up.set_ptrs(k, [t])
+        out = torch.zeros(3, device=dev)
+        up.set_clip_groups(1.0, 1e-6, tot, P, out=out)
+        up.sgd(torch.float32, 0.1, 0.0, 0.0, 0.0, False, False, True)
+        torch.cuda.synchronize()
+        assert out[0].item() == float(np.float32(_dpp_wave_sum(tot.cpu().numpy())))
+        assert abs(out[0].item() - exact) <= 1e-5 * exact
+
+
 _RED_FUSE_CHILD = r"""
 import sys, torch
 sys.path.insert(0, {repo!r})
