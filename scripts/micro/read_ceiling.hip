@@ -8,7 +8,9 @@
 // the chunk engine's streaming ops), resident grid-stride grids (2,048 and
 // 1,024 workgroups, as its capped reductions), cached or non-temporal loads,
 // with or without the reduction epilogue (block reduce through LDS + one store
-// per workgroup).  One JSON line per case.
+// per workgroup), and with the chunk engine's dependent scalar loads ahead of
+// every iteration's data loads (rd_tab).  The buffer holds hashed non-zero
+// values (the first run read zeros).  One JSON line per case.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -51,7 +53,53 @@ __global__ void __launch_bounds__(256) rd(const f4* __restrict__ x, int64_t n4, 
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
   } else {
-    if (acc == 12345.f) part[blockIdx.x] = acc;  // keeps the loads; never true here
+    if (acc == 12345.f) part[blockIdx.x] = acc;  // keeps the loads; (almost) never true
+  }
+}
+
+// The same grid-stride read, but every iteration first reads its group's place
+// through DEP dependent scalar loads, as the chunk engine does (chunk-table
+// entry, then the tensor's offset): tab[g] = g, off[t] = t * 256 * G float4s
+#define CONST_AS __attribute__((address_space(4)))
+template <int G, bool NT, int DEP>
+__global__ void __launch_bounds__(256) rd_tab(const f4* __restrict__ x, int64_t n4, float* __restrict__ part,
+                                              const int* tab, const int64_t* off) {
+  __shared__ float s[4];
+  float acc = 0.f;
+  const int64_t ngroups = (n4 + 256 * G - 1) / (256 * G);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int t = ((const CONST_AS int*)tab)[g];
+    const int64_t base = DEP >= 2 ? ((const CONST_AS int64_t*)off)[t] : (int64_t)t * 256 * G;
+    f4 v[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int64_t i = base + (int64_t)j * 256 + threadIdx.x;
+      v[j] = i < n4 ? ld<NT>(x + i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ void fill_tab(int* tab, int64_t* off, int64_t ng, int G) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < ng; i += (int64_t)gridDim.x * 256) {
+    tab[i] = (int)i;
+    off[i] = i * 256 * G;
+  }
+}
+
+// non-zero, incompressible-looking contents (an integer hash of the index)
+__global__ void fill(float* x, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint32_t h = (uint32_t)i * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    x[i] = ((float)(h & 0xFFFFFF) / 16777216.0f - 0.5f) * 0.02f;
   }
 }
 
@@ -61,7 +109,14 @@ int main() {
   f4* x;
   float* part;
   if (hipMalloc(&x, n * 4) || hipMalloc(&part, 65536 * 4)) return 1;
-  hipMemset(x, 0, n * 4);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (float*)x, n);
+  hipDeviceSynchronize();
+  int* tab;
+  int64_t* off;
+  const int64_t ng2 = (n4 + 511) / 512;
+  if (hipMalloc(&tab, ng2 * 4) || hipMalloc(&off, ng2 * 8)) return 1;
+  hipLaunchKernelGGL(fill_tab, dim3(256), dim3(256), 0, 0, tab, off, ng2, 2);
+  hipDeviceSynchronize();
   hipEvent_t a[50], b[50];
   for (int i = 0; i < 50; ++i) {
     hipEventCreate(&a[i]);
@@ -74,6 +129,21 @@ int main() {
   };
   std::vector<Case> cs;
   for (int round = 0; round < 2; ++round) {
+#define TCASE(NAME, NT, DEP)                                                                                  \
+  do {                                                                                                        \
+    for (int i = 0; i < 3; ++i)                                                                               \
+      hipLaunchKernelGGL((rd_tab<2, NT, DEP>), dim3(2048), dim3(256), 0, 0, x, n4, part, tab, off);           \
+    for (int i = 0; i < 50; ++i)                                                                              \
+      hipExtLaunchKernelGGL((rd_tab<2, NT, DEP>), dim3(2048), dim3(256), 0, 0, a[i], b[i], 0, x, n4, part, tab, \
+                            off);                                                                             \
+    hipDeviceSynchronize();                                                                                   \
+    std::vector<float> t(50);                                                                                 \
+    for (int i = 0; i < 50; ++i) hipEventElapsedTime(&t[i], a[i], b[i]);                                      \
+    float s = 0.f;                                                                                            \
+    for (float v : t) s += v;                                                                                 \
+    std::sort(t.begin(), t.end());                                                                            \
+    cs.push_back({NAME, 2048, s / 50, t[25]});                                                                \
+  } while (0)
 #define CASE(NAME, G, NT, RED, GRID)                                                                          \
   do {                                                                                                        \
     const int grid = (GRID) ? (GRID) : (int)((n4 + 256 * (G) - 1) / (256 * (G)));                            \
@@ -101,7 +171,12 @@ int main() {
     CASE("stride2k_g2_nt_red", 2, true, true, 2048);
     CASE("stride1k_g4_red", 4, false, true, 1024);
     CASE("stride1783_g2_red", 2, false, true, 1783);
+    TCASE("stride2k_g2_red_tab1", false, 1);
+    TCASE("stride2k_g2_red_tab2", false, 2);
+    TCASE("stride2k_g2_nt_red_tab1", true, 1);
+    TCASE("stride2k_g2_nt_red_tab2", true, 2);
 #undef CASE
+#undef TCASE
   }
   for (auto& c : cs) {
     const double gbps = 4.0 * n / (c.avg * 1e-3) / 1e9;
@@ -111,5 +186,7 @@ int main() {
   }
   hipFree(x);
   hipFree(part);
+  hipFree(tab);
+  hipFree(off);
   return 0;
 }
