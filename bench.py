@@ -472,8 +472,7 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
     torch.cuda.empty_cache()
     out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS, "iters": iters,
            "timing": "after the timed region, warm, alone on the GPU; plan launch timer (the kernels' own start "
-                     "and end: hipExtLaunchKernel's HIP events on the launch stream; GS_TIMER_EXT=0 = an event "
-                     f"pair around the launch), average of {iters} calls",
+                     f"and end: hipExtLaunchKernel's HIP events on the launch stream), average of {iters} calls",
            "min_frac": min(r["frac"] for r in rows.values()),
            "beyond_ic": {"params": n_big, "set": "ResNet-152 parameter shapes x 2 (> 256 MiB Infinity Cache)",
                          "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}

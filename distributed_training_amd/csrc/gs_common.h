@@ -183,7 +183,7 @@ struct gs_plan {
   std::vector<int64_t> voff;           // chunk-map engine: virtual offsets
   std::vector<gs::ChunkDesc> chunks;   // chunk-map engine: one per kChunkElems elements of voff space
   int grid = 0;
-  int grid_cap = gs::kMaxGrid;         // GS_MAX_GRID
+  int grid_cap = gs::kMaxGrid;         // the streaming ops' grid cap
   int64_t task_units = 0;
   // host shadow of the pointer table
   std::vector<void*> h_ptrs;       // [SLOTS * n]

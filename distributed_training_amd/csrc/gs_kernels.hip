@@ -335,8 +335,9 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
 // Σ x² of one slot left in the plan for a clipped update (gs_sqnorm_partial):
 // the chunk kernel with the in-kernel combine stopped at its 64 group sums
 // (no combine launch, no top-level hand-off); the update's workgroups fold them
-// (clip_multiplier).  The task engine (GS_ENGINE A/B runs) or an empty plan
-// writes the finished Σ into the plan's scalar word instead (red_groups = 0).
+// (clip_multiplier).  A reduction without the in-kernel combine (GS_RED_FUSE=0)
+// or an empty plan writes the finished Σ into the plan's scalar word instead
+// (red_groups = 0).
 const float* hip_plan_red_groups(const gs_plan* p) {
   return p->d_partials + kGridLimit + (kRedMaxGroups + 1) * kRedSyncStride;
 }
