@@ -8,8 +8,9 @@
 // the chunk engine's streaming ops), resident grid-stride grids (2,048 and
 // 1,024 workgroups, as its capped reductions), cached or non-temporal loads,
 // with or without the reduction epilogue (block reduce through LDS + one store
-// per workgroup), and with the chunk engine's dependent scalar loads ahead of
-// every iteration's data loads (rd_tab).  The buffer holds hashed non-zero
+// per workgroup), with the chunk engine's dependent scalar loads ahead of
+// every iteration's data loads (rd_tab), and with its two-level in-kernel
+// combine as the epilogue (rd_ticket).  The buffer holds hashed non-zero
 // values (the first run read zeros).  One JSON line per case.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -85,6 +86,76 @@ __global__ void __launch_bounds__(256) rd_tab(const f4* __restrict__ x, int64_t 
   if (threadIdx.x == 0) part[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
 
+// rd_tab<..., 2> with the chunk engine's in-kernel combine instead of the plain
+// store: the two-level ticket over R = 64 groups (gs_engine.h chunk_kernel: an
+// agent-scope store of the partial, vmcnt(0), an atomic add on the group's
+// counter; the group's last arriver folds the group, publishes its sum and
+// arrives on the top counter; the last group folds the 64 sums).
+template <bool NT>
+__global__ void __launch_bounds__(256) rd_ticket(const f4* __restrict__ x, int64_t n4, float* __restrict__ part,
+                                                 const int* tab, const int64_t* off, uint32_t* ticket,
+                                                 float* out) {
+  __shared__ float s[4];
+  __shared__ int s_role;
+  constexpr int G = 2, R = 64, kStride = 32;
+  float acc = 0.f;
+  const int64_t ngroups = (n4 + 256 * G - 1) / (256 * G);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int t = ((const CONST_AS int*)tab)[g];
+    const int64_t base = ((const CONST_AS int64_t*)off)[t];
+    f4 v[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int64_t i = base + (int64_t)j * 256 + threadIdx.x;
+      v[j] = i < n4 ? ld<NT>(x + i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float r = s[0] + s[1] + s[2] + s[3];
+  const int k = blockIdx.x & (R - 1);
+  const int grid = gridDim.x;
+  uint32_t* top = &ticket[R * kStride];
+  float* gsums = reinterpret_cast<float*>(ticket + (R + 1) * kStride);
+  if (threadIdx.x == 0) {
+    const uint32_t ng = (uint32_t)((grid - 1 - k) / R + 1);
+    __hip_atomic_store(&part[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t tk = __hip_atomic_fetch_add(&ticket[k * kStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_role = tk == ng - 1;
+  }
+  __syncthreads();
+  if (!s_role) return;
+  float v = 0.f;
+  for (int i = k + R * (int)threadIdx.x; i < grid; i += R * 256)
+    v += __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float gsum = s[0] + s[1] + s[2] + s[3];
+    __hip_atomic_store(&ticket[k * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&gsums[k * kStride], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t tk = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_role = tk == (uint32_t)(grid < R ? grid : R) - 1 ? 2 : 0;
+  }
+  __syncthreads();
+  if (s_role != 2 || threadIdx.x >= 64) return;
+  float t = 0.f;
+  for (int j = threadIdx.x; j < (grid < R ? grid : R); j += 64)
+    t += __hip_atomic_load(&gsums[j * kStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = wave_sum(t);
+  if (threadIdx.x == 0) {
+    out[0] = t;
+    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void fill_tab(int* tab, int64_t* off, int64_t ng, int G) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < ng; i += (int64_t)gridDim.x * 256) {
     tab[i] = (int)i;
@@ -117,6 +188,10 @@ int main() {
   if (hipMalloc(&tab, ng2 * 4) || hipMalloc(&off, ng2 * 8)) return 1;
   hipLaunchKernelGGL(fill_tab, dim3(256), dim3(256), 0, 0, tab, off, ng2, 2);
   hipDeviceSynchronize();
+  uint32_t* ticket;
+  float* outv;
+  if (hipMalloc(&ticket, 64 * 1024) || hipMalloc(&outv, 64)) return 1;
+  hipMemset(ticket, 0, 64 * 1024);
   hipEvent_t a[50], b[50];
   for (int i = 0; i < 50; ++i) {
     hipEventCreate(&a[i]);
@@ -136,6 +211,21 @@ int main() {
     for (int i = 0; i < 50; ++i)                                                                              \
       hipExtLaunchKernelGGL((rd_tab<2, NT, DEP>), dim3(2048), dim3(256), 0, 0, a[i], b[i], 0, x, n4, part, tab, \
                             off);                                                                             \
+    hipDeviceSynchronize();                                                                                   \
+    std::vector<float> t(50);                                                                                 \
+    for (int i = 0; i < 50; ++i) hipEventElapsedTime(&t[i], a[i], b[i]);                                      \
+    float s = 0.f;                                                                                            \
+    for (float v : t) s += v;                                                                                 \
+    std::sort(t.begin(), t.end());                                                                            \
+    cs.push_back({NAME, 2048, s / 50, t[25]});                                                                \
+  } while (0)
+#define KCASE(NAME, NT)                                                                                       \
+  do {                                                                                                        \
+    for (int i = 0; i < 3; ++i)                                                                               \
+      hipLaunchKernelGGL((rd_ticket<NT>), dim3(2048), dim3(256), 0, 0, x, n4, part, tab, off, ticket, outv);  \
+    for (int i = 0; i < 50; ++i)                                                                              \
+      hipExtLaunchKernelGGL((rd_ticket<NT>), dim3(2048), dim3(256), 0, 0, a[i], b[i], 0, x, n4, part, tab, off, \
+                            ticket, outv);                                                                    \
     hipDeviceSynchronize();                                                                                   \
     std::vector<float> t(50);                                                                                 \
     for (int i = 0; i < 50; ++i) hipEventElapsedTime(&t[i], a[i], b[i]);                                      \
@@ -175,7 +265,10 @@ int main() {
     TCASE("stride2k_g2_red_tab2", false, 2);
     TCASE("stride2k_g2_nt_red_tab1", true, 1);
     TCASE("stride2k_g2_nt_red_tab2", true, 2);
+    KCASE("stride2k_g2_tab2_ticket", false);
+    KCASE("stride2k_g2_nt_tab2_ticket", true);
 #undef CASE
+#undef KCASE
 #undef TCASE
   }
   for (auto& c : cs) {
@@ -188,5 +281,7 @@ int main() {
   hipFree(part);
   hipFree(tab);
   hipFree(off);
+  hipFree(ticket);
+  hipFree(outv);
   return 0;
 }
