@@ -9,8 +9,9 @@
 // 1,024 workgroups, as its capped reductions), cached or non-temporal loads,
 // with or without the reduction epilogue (block reduce through LDS + one store
 // per workgroup), with the chunk engine's dependent scalar loads ahead of
-// every iteration's data loads (rd_tab), and with its two-level in-kernel
-// combine as the epilogue (rd_ticket).  The buffer holds hashed non-zero
+// every iteration's data loads (rd_tab), with its two-level in-kernel combine
+// as the epilogue (rd_ticket), and with a polling combiner (rd_poll, checked
+// against the host's double sum).  The buffer holds hashed non-zero
 // values (the first run read zeros).  One JSON line per case.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -156,6 +157,73 @@ __global__ void __launch_bounds__(256) rd_ticket(const f4* __restrict__ x, int64
   }
 }
 
+// The same with a polling combiner instead of the last-arriver hand-offs:
+// every other workgroup stores its partial (sc1), drains it and adds to its
+// group's counter without waiting for the add (64 counters, one 128-B line
+// each); workgroup 0, after its own data, polls the 64 counters (one per lane
+// of wave 0, sc1 loads) until every group has arrived, re-arms them and folds
+// all partials in a fixed order.  The spin is bounded (kPollMax polls, then
+// the result is NaN) so that a lost arrival cannot hang the GPU.
+constexpr int kPollMax = 1 << 22;
+template <bool NT>
+__global__ void __launch_bounds__(256) rd_poll(const f4* __restrict__ x, int64_t n4, float* __restrict__ part,
+                                               const int* tab, const int64_t* off, uint32_t* ticket, float* out) {
+  __shared__ float s[4];
+  __shared__ int s_ok;
+  constexpr int G = 2, R = 64, kStride = 32;
+  float acc = 0.f;
+  const int64_t ngroups = (n4 + 256 * G - 1) / (256 * G);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int t = ((const CONST_AS int*)tab)[g];
+    const int64_t base = ((const CONST_AS int64_t*)off)[t];
+    f4 v[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int64_t i = base + (int64_t)j * 256 + threadIdx.x;
+      v[j] = i < n4 ? ld<NT>(x + i) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc += v[j].x * v[j].x + v[j].y * v[j].y + v[j].z * v[j].z + v[j].w * v[j].w;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float r = s[0] + s[1] + s[2] + s[3];
+  const int grid = gridDim.x;
+  if (blockIdx.x != 0) {
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&part[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&ticket[(blockIdx.x & (R - 1)) * kStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    const uint32_t want = j < grid ? (uint32_t)((grid - 1 - j) / R + 1) - (j == 0 ? 1u : 0u) : 0u;
+    int ok = 0;
+    for (int it = 0; it < kPollMax; ++it) {
+      const uint32_t c = __hip_atomic_load(&ticket[j * kStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(c >= want)) {
+        ok = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(&ticket[j * kStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j == 0) s_ok = ok;
+  }
+  __syncthreads();
+  float v = 0.f;
+  for (int i = threadIdx.x; i < grid; i += 256)
+    v += i == 0 ? r : __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = s_ok ? s[0] + s[1] + s[2] + s[3] : __builtin_nanf("");
+}
+
 __global__ void fill_tab(int* tab, int64_t* off, int64_t ng, int G) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < ng; i += (int64_t)gridDim.x * 256) {
     tab[i] = (int)i;
@@ -192,6 +260,12 @@ int main() {
   float* outv;
   if (hipMalloc(&ticket, 64 * 1024) || hipMalloc(&outv, 64)) return 1;
   hipMemset(ticket, 0, 64 * 1024);
+  double ref = 0.0;
+  {
+    std::vector<float> h(n);
+    hipMemcpy(h.data(), x, n * 4, hipMemcpyDeviceToHost);
+    for (float v : h) ref += (double)v * v;
+  }
   hipEvent_t a[50], b[50];
   for (int i = 0; i < 50; ++i) {
     hipEventCreate(&a[i]);
@@ -234,6 +308,24 @@ int main() {
     std::sort(t.begin(), t.end());                                                                            \
     cs.push_back({NAME, 2048, s / 50, t[25]});                                                                \
   } while (0)
+#define PCASE(NAME, NT)                                                                                       \
+  do {                                                                                                        \
+    for (int i = 0; i < 3; ++i)                                                                               \
+      hipLaunchKernelGGL((rd_poll<NT>), dim3(2048), dim3(256), 0, 0, x, n4, part, tab, off, ticket, outv);    \
+    for (int i = 0; i < 50; ++i)                                                                              \
+      hipExtLaunchKernelGGL((rd_poll<NT>), dim3(2048), dim3(256), 0, 0, a[i], b[i], 0, x, n4, part, tab, off, \
+                            ticket, outv);                                                                    \
+    if (hipDeviceSynchronize() != hipSuccess) return 2;                                                       \
+    std::vector<float> t(50);                                                                                 \
+    for (int i = 0; i < 50; ++i) hipEventElapsedTime(&t[i], a[i], b[i]);                                      \
+    float s = 0.f;                                                                                            \
+    for (float v : t) s += v;                                                                                 \
+    std::sort(t.begin(), t.end());                                                                            \
+    cs.push_back({NAME, 2048, s / 50, t[25]});                                                                \
+    float o = 0.f;                                                                                            \
+    hipMemcpy(&o, outv, 4, hipMemcpyDeviceToHost);                                                            \
+    printf("{\"check\": \"%s\", \"sum\": %.6e, \"ref\": %.6e}\n", NAME, o, ref);                            \
+  } while (0)
 #define CASE(NAME, G, NT, RED, GRID)                                                                          \
   do {                                                                                                        \
     const int grid = (GRID) ? (GRID) : (int)((n4 + 256 * (G) - 1) / (256 * (G)));                            \
@@ -267,7 +359,10 @@ int main() {
     TCASE("stride2k_g2_nt_red_tab2", true, 2);
     KCASE("stride2k_g2_tab2_ticket", false);
     KCASE("stride2k_g2_nt_tab2_ticket", true);
+    PCASE("stride2k_g2_tab2_poll", false);
+    PCASE("stride2k_g2_nt_tab2_poll", true);
 #undef CASE
+#undef PCASE
 #undef KCASE
 #undef TCASE
   }
