@@ -29,7 +29,11 @@ namespace gs {
 ncclComm_t comm_handle(gs_comm* c);
 hipStream_t comm_stream(gs_comm* c);
 int comm_dtype(int dt, ncclDataType_t* out);
-int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what);
+int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what,
+                 bool track = true);
+int comm_track_event(gs_comm* c, hipEvent_t ev);
+bool comm_watching(gs_comm* c);
+void comm_forget_event(gs_comm* c, hipEvent_t ev);
 }  // namespace gs
 
 using namespace gs;
@@ -59,6 +63,7 @@ struct Bucket {
   // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
   hipEvent_t ev_sync = nullptr;  // untimed ready event (a comm-stream chain waits on it)
+  hipEvent_t ev_wd = nullptr;    // the watchdog's mark of the collective, carried by the unpack kernel
   bool timed = false;            // pk0 / t0 / t1 / u1 recorded (level 2)
   bool pk0_is_ready = false;     // the producer-side tail: its pack follows the ready mark on the same
                                  // stream with nothing between, so ready doubles as pk0 (queue 0)
@@ -217,7 +222,9 @@ int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
   return debug_sum(b, bk, 0, stream);
 }
 
-int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
+// track = false: the caller hands the collective to the watchdog through an event
+// of its own that the stream records after it (comm_track_event)
+int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs, bool track = true) {
   ncclDataType_t dt;
   GS_TRY_RET(comm_dtype(bk.bdt, &dt));
   if (b->flags & GS_BKT_REDUCE_SCATTER) {
@@ -225,11 +232,11 @@ int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs) {
     return comm_enqueue(b->comm, cs, [&] {
       return ncclReduceScatter(bk.buf, bk.shard, static_cast<size_t>(bk.numel / w), dt, ncclSum,
                                comm_handle(b->comm), cs);
-    }, "bucket reduce-scatter");
+    }, "bucket reduce-scatter", track);
   }
   return comm_enqueue(b->comm, cs, [&] {
     return ncclAllReduce(bk.buf, bk.buf, static_cast<size_t>(bk.numel), dt, ncclSum, comm_handle(b->comm), cs);
-  }, "bucket all-reduce");
+  }, "bucket all-reduce", track);
 }
 
 int launch_bucket(gs_bucketer* b, int bi) {
@@ -300,13 +307,21 @@ int launch_bucket(gs_bucketer* b, int bi) {
     }
     GS_TRY_RET(debug_sum(b, bk, 0, cs));
     if (on_producer && bi > 0) HIPB_RET(hipStreamWaitEvent(ps, b->ev_comm, 0));
-    GS_TRY_RET(launch_collective(b, bk, cs));
+    // The watchdog learns of the collective's completion through the stop event its
+    // unpack kernel carries (the done mark, u1, or ev_wd), not through an event packet
+    // after the collective: a packet costs ~4.7 µs of stream time, a kernel-carried
+    // stop ~2.4 (scripts/micro/event_chain.hip) — the whole gap between the tail's
+    // pack and unpack at N = 1 (scripts/tail_trace.py)
+    const bool unpacks = b->do_unpack() || b->found_inf;
+    hipEvent_t wd_ev = (!capturing && unpacks && comm_watching(b->comm)) ? (end_ev ? end_ev : bk.ev_wd) : nullptr;
+    GS_TRY_RET(launch_collective(b, bk, cs, wd_ev == nullptr));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
     // unpack: t1 a packet before it, its stop = u1 or the done mark; the collective lies
     // between t0 and t1
-    if (b->do_unpack() || b->found_inf) {
+    if (unpacks) {
       if (timed) HIPB_RET(hipEventRecord(bk.ev_t1, cs));
-      GS_TRY_RET(unpack_one(b, bk, cs, 0, nullptr, end_ev));
+      GS_TRY_RET(unpack_one(b, bk, cs, 0, nullptr, wd_ev ? wd_ev : end_ev));
+      if (wd_ev) GS_TRY_RET(comm_track_event(b->comm, wd_ev));
     } else if (timed) {
       HIPB_RET(hipEventRecord(bk.ev_t1, cs));
       HIPB_RET(hipEventRecord(bk.ev_u1, cs));
@@ -402,7 +417,8 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
       if (hipEventCreate(&bk.ev_ready) != hipSuccess || hipEventCreate(&bk.ev_pk0) != hipSuccess ||
           hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess ||
           hipEventCreate(&bk.ev_u1) != hipSuccess ||
-          hipEventCreateWithFlags(&bk.ev_sync, hipEventDisableTiming) != hipSuccess)
+          hipEventCreateWithFlags(&bk.ev_sync, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&bk.ev_wd, hipEventDisableTiming) != hipSuccess)
         return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
     }
   }
@@ -421,10 +437,17 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
 int gs_bucketer_destroy(gs_bucketer* b) {
   if (!b) return GS_OK;
   if (b->hip() && b->comm) (void)hipStreamSynchronize(comm_stream(b->comm));
+  if (b->hip() && b->comm) {  // the watchdog may still hold the tail's marks (comm_track_event)
+    comm_forget_event(b->comm, b->ev_done);
+    for (Bucket& bk : b->buckets) {
+      comm_forget_event(b->comm, bk.ev_u1);
+      comm_forget_event(b->comm, bk.ev_wd);
+    }
+  }
   for (Bucket& bk : b->buckets) {
     gs_plan_destroy(bk.plan);
     gs_plan_destroy(bk.flat);
-    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1, bk.ev_sync})
+    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1, bk.ev_sync, bk.ev_wd})
       if (ev) (void)hipEventDestroy(ev);
   }
   if (b->ev_done) (void)hipEventDestroy(b->ev_done);

@@ -45,6 +45,7 @@ struct gs_comm {
   struct Inflight {
     hipEvent_t ev;
     std::chrono::steady_clock::time_point t0;
+    bool pooled;  // from ev_pool (a packet after the collective) or the caller's (comm_track_event)
   };
   std::deque<Inflight> inflight;
   std::vector<hipEvent_t> ev_pool;
@@ -158,7 +159,7 @@ void watchdog_loop(gs_comm* c) {
       continue;
     }
     while (!c->inflight.empty() && hipEventQuery(c->inflight.front().ev) == hipSuccess) {
-      c->ev_pool.push_back(c->inflight.front().ev);
+      if (c->inflight.front().pooled) c->ev_pool.push_back(c->inflight.front().ev);
       c->inflight.pop_front();
     }
     if (!c->inflight.empty() && c->timeout_ms > 0) {
@@ -193,13 +194,40 @@ int comm_track_locked(gs_comm* c, hipStream_t stream) {
     c->ev_pool.push_back(ev);
     return fail(GS_EHIP, "watchdog: event record failed");
   }
-  c->inflight.push_back({ev, std::chrono::steady_clock::now()});
+  c->inflight.push_back({ev, std::chrono::steady_clock::now(), true});
   return GS_OK;
+}
+
+// A collective enqueued untracked (comm_enqueue track = false) handed to the
+// watchdog through an event of the caller's that its stream records after it —
+// the bucketer: each bucket's unpack kernel carries the stop event, so no event
+// packet sits between a collective and its unpack (~4.7 µs of stream time each,
+// scripts/micro/event_chain.hip).  The caller keeps the event
+// and calls comm_forget_event before destroying it.
+int comm_track_event(gs_comm* c, hipEvent_t ev) {
+  if (!c || !ev) return GS_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->timeout_ms <= 0) return GS_OK;
+  c->inflight.push_back({ev, std::chrono::steady_clock::now(), false});
+  return GS_OK;
+}
+
+bool comm_watching(gs_comm* c) {
+  if (!c) return false;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->timeout_ms > 0;
+}
+
+void comm_forget_event(gs_comm* c, hipEvent_t ev) {
+  if (!c || !ev) return;
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (auto it = c->inflight.begin(); it != c->inflight.end();) it = it->ev == ev ? c->inflight.erase(it) : it + 1;
 }
 
 // Enqueue one RCCL collective under c->mu: liveness check, enqueue and
 // watchdog tracking are atomic with respect to the watchdog's abort.
-int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what) {
+int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what,
+                 bool track = true) {
   if (!c) return fail(GS_EINVAL, "no communicator");
   GsRange range(what);
   std::lock_guard<std::mutex> lk(c->mu);
@@ -208,7 +236,7 @@ int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_
   const ncclResult_t r = fn();
   c->enq_since.store(0);
   if (r != ncclSuccess) return rccl_fail(r, what);
-  return comm_track_locked(c, stream);
+  return track ? comm_track_locked(c, stream) : GS_OK;
 }
 
 }  // namespace gs
@@ -275,7 +303,8 @@ int gs_comm_destroy(gs_comm* c) {
   }
   (void)hipSetDevice(c->device);
   if (c->stream && !c->aborted.load()) (void)hipStreamSynchronize(c->stream);
-  for (auto& f : c->inflight) (void)hipEventDestroy(f.ev);
+  for (auto& f : c->inflight)
+    if (f.pooled) (void)hipEventDestroy(f.ev);  // the caller's events stay the caller's
   for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
   if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);

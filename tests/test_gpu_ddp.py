@@ -458,6 +458,48 @@ def test_communicator_watchdog_and_abort(cuda_device):
     c.close()
 
 
+def test_ddp_watchdog_marks_on_unpacks(cuda_device, rccl_pg):
+    """The bucketer hands each collective to the RCCL watchdog through the stop
+    event its unpack kernel carries (no event packet after the collective): with
+    a 400 ms timeout, steps at timeline levels 0, 1 and 2 complete, and after a
+    wait longer than the timeout nothing counts as hung; closing the DDP drops
+    the bucketer's events from the watchdog; the grads equal the hooks' own at
+    world size 1."""
+    import time
+
+    from distributed_training_amd import DistributedDataParallel
+    from distributed_training_amd.resnet import micro_resnet
+
+    torch.manual_seed(0)
+    model = micro_resnet().to(cuda_device).to(memory_format=torch.channels_last)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model)
+    comm = ddp._comm
+    saved = comm.timeout_ms
+    comm.set_timeout(400)
+    g = torch.Generator(device=cuda_device).manual_seed(3)
+    for level in (0, 1, 2, 1):
+        ddp.set_timeline(level)
+        x = torch.rand(8, 3, 32, 32, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (8,), device=cuda_device, generator=g)
+        for p in params:
+            p.grad = None
+        torch.nn.functional.cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        for i, p in enumerate(params):
+            assert torch.equal(p.grad, local[i]), f"level {level} param {i}"
+    time.sleep(0.6)
+    assert comm.status() == (False, "")
+    own = getattr(ddp, "_own_comm", False)
+    ddp.close()  # drops the bucketer's events from the watchdog before destroying them
+    if not own:  # a shared communicator lives on: its watchdog must not trip on them
+        time.sleep(0.6)
+        assert comm.status() == (False, "")
+        comm.set_timeout(saved)
+
+
 @pytest.mark.parametrize("kind", ["sgd", "adamw"])
 def test_overlapped_optimizer_ws1_rccl(cuda_device, rccl_pg, kind):
     """DDP._register_fused_optim on the AUTO-collective path: each bucket's
