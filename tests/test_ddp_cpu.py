@@ -2,6 +2,7 @@
 configuration-1 plumbing path (BASELINE.json configs[0]), compared with the
 golden fixtures of the reference's own DDP train step and with torch's DDP
 run side by side."""
+import gc
 import os
 
 import numpy as np
@@ -42,12 +43,24 @@ def _wrap(fn, rank, ws, port, errq, *args):
     import faulthandler
 
     faulthandler.enable(all_threads=True)
+    if os.environ.get("GSYNC_TERMINATE_TRACE"):  # diagnosis: native backtrace of an exit-time abort
+        import ctypes
+
+        ctypes.CDLL(os.environ["GSYNC_TERMINATE_TRACE"])
     try:
         init_pg("gloo", rank, ws, port)
         torch.set_num_threads(max(1, 8 // ws))  # as make_golden.py: CPU conv sums depend on it
         fn(rank, ws, *args)
+        # Free the test's objects (a DDP in a reference cycle holds the process group)
+        # while the interpreter is whole: a gloo worker thread that drops the last
+        # reference to a Python-owned tensor during interpreter finalization cannot
+        # take the GIL and ends in std::terminate (ProcessGroupGloo::runLoop ->
+        # TensorImpl::decref_pyobject -> pthread_exit under a noexcept frame; native
+        # backtrace with GSYNC_TERMINATE_TRACE)
+        gc.collect()
         dist.barrier()  # no rank tears gloo down while a peer is still talking
         dist.destroy_process_group()
+        gc.collect()
     except BaseException as e:
         import traceback
 

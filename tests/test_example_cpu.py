@@ -58,6 +58,9 @@ def _reference(rank, ws, port, steps, batch, n, q):
         out = {k: v.detach().numpy().copy() for k, v in model.module.state_dict().items()}
         out.update(grads)
         q.put(out)
+    import gc
+
+    gc.collect()  # as tests/test_ddp_cpu.py::_wrap: no gloo work outlives the interpreter
     dist.destroy_process_group()
 
 

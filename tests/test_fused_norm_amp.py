@@ -149,6 +149,9 @@ def _gpu_worker(rank, ws, port, errq):
         from distributed_training_amd.comm import destroy_communicators
 
         destroy_communicators()
+        import gc
+
+        gc.collect()  # as tests/test_ddp_cpu.py::_wrap: no gloo work outlives the interpreter
         dist.destroy_process_group()
     except BaseException as e:
         import traceback
