@@ -1434,6 +1434,12 @@ def main():
     if watchdog is not None:
         watchdog.cancel()
 
+    # free the engines (reference cycles hold the process group) before the teardown:
+    # a gloo worker thread dropping a Python tensor during interpreter finalization
+    # ends in std::terminate
+    import gc
+
+    gc.collect()
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -1471,3 +1477,6 @@ def main():
 
 if __name__ == "__main__":
     main()
+    import gc
+
+    gc.collect()  # main()'s engines are unreachable now: their process group goes before finalization

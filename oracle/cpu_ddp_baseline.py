@@ -72,6 +72,14 @@ def worker(rank, args, q):
     ar_s = (time.perf_counter() - t0) / args.ar_iters
     if rank == 0:
         q.put((times, ar_s, nparam * 4))
+    # torch's DDP here sits in a reference cycle that holds the process group: free it
+    # before the teardown, so no gloo worker thread drops a Python tensor during
+    # interpreter finalization (std::terminate)
+    del model, optimizer, buf
+    import gc
+
+    gc.collect()
+    dist.barrier()
     dist.destroy_process_group()
 
 
