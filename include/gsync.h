@@ -106,7 +106,11 @@ int gs_comm_abort(gs_comm* c);
 /* failure detection: with timeout_ms > 0 a watchdog thread aborts the
  * communicator (ncclCommAbort) when a collective enqueued through it has been
  * in flight longer than timeout_ms, or RCCL reports an asynchronous error;
- * later calls then fail with GS_ERCCL.  0 disables the timeout.
+ * later calls then fail with GS_ERCCL.  0 disables the timeout.  A
+ * collective called through this API is followed by an event on its stream
+ * for the watchdog to poll; the bucketer's collectives are instead watched
+ * through the stop event their unpack kernel carries (no event packet between
+ * a bucket's collective and its unpack).
  * replaces: ProcessGroupNCCL's watchdog / TORCH_NCCL_ASYNC_ERROR_HANDLING
  *           (T:include/torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp:59-68, :156) */
 int gs_comm_set_timeout(gs_comm* c, int64_t timeout_ms);
