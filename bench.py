@@ -478,6 +478,53 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
                          "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}
     if comm is not None and world == 1:
         out.update(zero_clip_path_rows(n, dev, comm, iters=iters))
+    out["beyond_ic"]["plain_stream_ceiling_live"] = _live_mix_ceiling(dev)
+    return out
+
+
+# the update rows' mixes as scripts/micro/stream_mix.hip names its plain-stream cases
+LIVE_MIX_CASES = {"sgd3r2w": ("sgd3r2w_g2", "sgd3r2w_g4", "sgd3r2w_g4_ntl"),
+                  "adam4r3w": ("adam4r3w_g4", "adam4r3w_g4_ntl")}
+
+
+def _live_mix_ceiling(dev):
+    """The plain-stream ceiling of the update rows' read / write mixes measured on
+    THIS box, right after the beyond-cache rows: scripts/micro/stream_mix (built
+    in-tree by __graft_entry__.build()) as a child process on the same GPU, the
+    mix's one-shot-grid cases on ResNet-152 x 2 elements, each kernel timed by
+    its own start / stop events like the plan launch timer; per mix the best case
+    (median of 2 rounds x 20 launches).  None (with the reason) when the binary is
+    absent or fails."""
+    import subprocess
+
+    exe = os.path.join(REPO, "scripts", "micro", "stream_mix")
+    if not os.path.exists(exe):
+        return {"error": "scripts/micro/stream_mix not built"}
+    if (dev.index or 0) != 0:  # the child runs on its default device: the same GPU only for device 0
+        return {"error": f"measured on device 0 only (this rank: {dev})"}
+    torch.cuda.synchronize(dev)
+    cases = [c for cs in LIVE_MIX_CASES.values() for c in cs]
+    try:
+        p = subprocess.run([exe] + cases, capture_output=True, text=True, timeout=120)
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return {"error": f"stream_mix: {e!r}"}
+    if p.returncode != 0:
+        return {"error": f"stream_mix exit {p.returncode}: {p.stderr[-300:]}"}
+    rows = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    out = {}
+    for mix, names in LIVE_MIX_CASES.items():
+        per = {}
+        for r in rows:
+            if r["case"] in names:
+                per.setdefault(r["case"], []).append(r["frac"])
+        if per:
+            best = max(per, key=lambda c: sorted(per[c])[len(per[c]) // 2])
+            fr = sorted(per[best])[len(per[best]) // 2]
+            out[mix] = {"frac": round(fr, 4), "GBps": round(fr * HBM_PEAK_GBPS, 1), "case": best,
+                        "cases": {c: [round(x, 4) for x in v] for c, v in per.items()}}
+    out["source"] = ("scripts/micro/stream_mix.hip run live on this GPU after the beyond-cache rows: a plain float4 "
+                     "grid of the same read / write mix on the same 120.4 M elements, no chunk map; kernel start / "
+                     "stop events")
     return out
 
 
@@ -1178,6 +1225,13 @@ def main():
         if bic:
             r["frac_beyond_ic"] = bic["frac"]
             r["plain_stream_ceiling"] = bic["plain_stream_ceiling"]
+            live = (kernel_rates or {}).get("beyond_ic", {}).get("plain_stream_ceiling_live") or {}
+            mix = live.get("sgd3r2w" if args.optimizer == "sgd" else "adam4r3w")
+            if mix:
+                r["plain_stream_ceiling_live"] = dict(mix, source=live.get("source"))
+                r["frac_of_live_ceiling"] = bic["frac"] / mix["frac"] if mix["frac"] else None
+            elif live.get("error"):
+                r["plain_stream_ceiling_live"] = {"error": live["error"]}
             if "rocprof" in bic:
                 r["rocprof"] = bic["rocprof"]
             r["in_step"] = in_step

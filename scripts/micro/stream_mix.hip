@@ -7,10 +7,14 @@
 // one-shot grid (one G-group per workgroup, as libgsync's chunk engine) or a
 // resident grid-stride grid.  ResNet-152 x 2 elements (120.4 M, 2.4 GB per SGD
 // launch: > 9x the 256 MiB cache), back-to-back launches timed by an event pair
-// each (the beyond_ic harness's conditions).  One JSON line per case.
+// each (the beyond_ic harness's conditions).  One JSON line per case.  With case
+// names as arguments: only those cases on the one-shot grid, each kernel timed
+// by its own start / stop events (bench.py's live ceiling for the update rows).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -82,17 +86,26 @@ __global__ void __launch_bounds__(256) mix(f4* __restrict__ s0, f4* __restrict__
   }
 }
 
+// launch(a, b): a null pair = a plain launch; else the kernel carries a / b as its
+// own start / stop events (hipExtLaunchKernel, as libgsync's plan launch timer
+// times its kernels) — the mode with case names on the command line; without
+// them, an event pair of packets around each launch (the committed r4 runs)
+static bool g_ext = false;
 template <class K>
 static float time_ms(K launch, int iters) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int i = 0; i < 3; ++i) launch();
+  for (int i = 0; i < 3; ++i) launch(nullptr, nullptr);
   float tot = 0.f;
   for (int i = 0; i < iters; ++i) {
-    hipEventRecord(a, 0);
-    launch();
-    hipEventRecord(b, 0);
+    if (g_ext) {
+      launch(a, b);
+    } else {
+      hipEventRecord(a, 0);
+      launch(nullptr, nullptr);
+      hipEventRecord(b, 0);
+    }
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
@@ -103,7 +116,17 @@ static float time_ms(K launch, int iters) {
   return tot / iters;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // optional: case names to run (only those, grid 0 and both rounds), ext-event timing
+  std::vector<std::string> only(argv + 1, argv + argc);
+  g_ext = !only.empty();
+  auto wanted = [&](const char* name, int gridc) {
+    if (only.empty()) return true;
+    if (gridc != 0) return false;
+    for (auto& o : only)
+      if (o == name) return true;
+    return false;
+  };
   const int64_t n = 120385616 / 1024 * 1024;  // ResNet-152 x 2, whole 1 Ki chunks
   const int64_t n4 = n / 4;
   f4* s[4];
@@ -127,9 +150,15 @@ int main() {
     for (int gridc : {0, 2048, 8192}) {
       auto g_of = [&](int G) { return gridc ? gridc : (int)std::min<int64_t>(1 << 30, (n4 + 256 * G - 1) / (256 * G)); };
 #define CASE(NAME, BPE, R, W, G, NTL, NTS, ...)                                                                      \
+  if (wanted(NAME, gridc))                                                                                           \
   cs.push_back({NAME, BPE,                                                                                           \
-                time_ms([&] { mix<R, W, G, NTL, NTS, ##__VA_ARGS__><<<g_of(G), 256>>>(s[0], s[1], s[2], s[3], n4, part); }, \
-                        20),                                                                                         \
+                time_ms([&](hipEvent_t ea, hipEvent_t eb) {                                                          \
+                  if (ea)                                                                                            \
+                    hipExtLaunchKernelGGL((mix<R, W, G, NTL, NTS, ##__VA_ARGS__>), dim3(g_of(G)), dim3(256), 0, 0,   \
+                                          ea, eb, 0, s[0], s[1], s[2], s[3], n4, part);                              \
+                  else                                                                                               \
+                    mix<R, W, G, NTL, NTS, ##__VA_ARGS__><<<g_of(G), 256>>>(s[0], s[1], s[2], s[3], n4, part);       \
+                }, 20),                                                                                              \
                 gridc})
       CASE("read_sum_g4", 4, 1, 0, 4, false, true);
       CASE("read_sum_g4_ntl", 4, 1, 0, 4, true, true);

@@ -163,6 +163,11 @@ def _check_line(d, n):
     assert r["frac_of_copy_ceiling"] <= 1.1  # a true-HBM figure: not above the copy ceiling (box spread aside)
     # ... read against a plain float4 stream of the same 3R2W mix (committed probe run)
     assert r["plain_stream_ceiling"]["case"].startswith("sgd3r2w")
+    # ... and against the same probe run live on this GPU (stream_mix as a child process)
+    live = r["plain_stream_ceiling_live"]
+    assert "error" not in live, live
+    assert live["case"].startswith("sgd3r2w") and 0.3 < live["frac"] < 1.0
+    assert abs(r["frac_of_live_ceiling"] - r["frac"] / live["frac"]) < 1e-9
     if n == 1:  # configs[3]'s N>1 clip path at its N=8 shard, over the one-rank RCCL communicator
         z, zs = k["clip_path_zero_n8"], k["clip_path_zero_n8_scalar"]
         assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > 0 and z["kernels_ms"] > 0
