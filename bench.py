@@ -478,13 +478,21 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
                          "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}
     if comm is not None and world == 1:
         out.update(zero_clip_path_rows(n, dev, comm, iters=iters))
-    out["beyond_ic"]["plain_stream_ceiling_live"] = _live_mix_ceiling(dev)
+    live = _live_mix_ceiling(dev)
+    out["beyond_ic"]["plain_stream_ceiling_live"] = live
+    for name, mix in LIVE_MIX_OF_ROW.items():  # each row against its own mix's plain grid
+        if name in big and (live.get(mix) or {}).get("frac"):
+            big[name]["frac_of_live_ceiling"] = big[name]["frac"] / live[mix]["frac"]
     return out
 
 
 # the update rows' mixes as scripts/micro/stream_mix.hip names its plain-stream cases
 LIVE_MIX_CASES = {"sgd3r2w": ("sgd3r2w_g2", "sgd3r2w_g4", "sgd3r2w_g4_ntl"),
-                  "adam4r3w": ("adam4r3w_g4", "adam4r3w_g4_ntl")}
+                  "adam4r3w": ("adam4r3w_g4", "adam4r3w_g4_ntl"),
+                  "copy": ("copy_g4", "copy_g4_ntl"), "read": ("read_sum_g4", "read_sum_g4_ntl")}
+# the beyond-cache rows whose stream mix one of them is exactly (fp32 throughout)
+LIVE_MIX_OF_ROW = {"sgd_momentum_wd": "sgd3r2w", "adam": "adam4r3w", "pack_f32": "copy", "unpack_f32": "copy",
+                   "sqnorm_f32": "read", "sqnorm_partial_f32": "read"}
 
 
 def _live_mix_ceiling(dev):
