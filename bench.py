@@ -235,6 +235,27 @@ def _kernel_rows(shapes, dev, iters):
             ("sqnorm_f32", 4 * n, lambda: plan.sqnorm(1, torch.float32, sq))):
         ms = rate(fn, plan)
         rows[name] = {"alg_bytes": nbytes, "avg_ms": ms, "GBps": nbytes / (ms * 1e-3) / 1e9}
+    # Σg² as a clip after a libgsync DDP runs it: its first read of grads the unpack has
+    # just written with non-temporal stores (per iteration: the unpack, then Σg²; the
+    # Σg² launches alone timed), under the default load rule and the non-temporal hint
+    # (gs_plan_set_read_hint) — the looped row above reads grads its own previous pass
+    # left in the cache
+    from distributed_training_amd import _lib as L
+
+    for name, hint in (("sqnorm_f32_after_unpack", 0), ("sqnorm_f32_after_unpack_nt", 1)):
+        plan.set_read_hint(hint)
+        for _ in range(3):
+            plan.unpack(flat, 1, torch.float32)
+            plan.sqnorm(1, torch.float32, sq)
+        plan.timer_enable(4 * iters)
+        for _ in range(iters):
+            plan.unpack(flat, 1, torch.float32)
+            plan.sqnorm(1, torch.float32, sq)
+        ms = sum(plan.timer_read_by_kind().get(L.GS_OP_SQNORM, [])) / iters
+        plan.timer_enable(0)
+        rows[name] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9,
+                      "read_hint": "the size rule (cached below 256 MiB)" if hint == 0 else "non-temporal"}
+    plan.set_read_hint(0)
     # the 16-bit bucket paths: ZeRO's bf16 grads -> bf16 bucket (configs[3]) and the bf16
     # bucket -> fp32 grads unpack (DDP bucket_dtype=bf16)
     grads16 = [gr.to(torch.bfloat16) for gr in grads]

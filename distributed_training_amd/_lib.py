@@ -101,6 +101,7 @@ SIGNATURES = {
     "gs_sum": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp]),
     "gs_sqnorm_partial": (_c_int, [_vp, _c_int, _c_int, _vp]),
     "gs_plan_set_clip": (_c_int, [_vp, _vp, _c_f, _c_f, _c_f, _c_f, _vp]),
+    "gs_plan_set_read_hint": (_c_int, [_vp, _c_int]),
     "gs_sqnorm_partial_out": (_c_int, [_vp, _c_int, _c_int, _vp, _p_i32, _vp]),
     "gs_plan_set_clip_groups": (_c_int, [_vp, _vp, ctypes.c_int32, _c_f, _c_f, _c_f, _c_f, _vp]),
     "gs_rng_state_bytes": (_c_int, []),

@@ -213,6 +213,7 @@ struct gs_plan {
   int red_groups = 0;
   bool red_valid = false;       // a gs_sqnorm_partial has run on this plan
   bool grads_read = false;      // a Σg² pass read slot 1 since the last update (load policy)
+  int read_hint = 0;            // Σg² loads: 0 the size rule, 1 non-temporal, 2 cached (gs_plan_set_read_hint)
   float h_red = 0.f;            // host plans: the Σg² of gs_sqnorm_partial
   // launch timer ring (gs_plan_timer_enable)
   std::vector<void*> timer_ev;  // [2 * slots]: start, stop

@@ -130,7 +130,9 @@ constexpr int64_t kInfinityCacheBytes = 256ll << 20;
 // than NT loads, the Σg² folded into the unpack (fuse_grad_norm_into).
 // GS_NT_READ_ONCE / GS_NT_SQNORM (environment): 0 never, 1 always, 2 the size rule
 // (default) — tests/test_clip_fold.py checks that no policy changes a bit.
-inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
+// hint (gs_plan_set_read_hint, Σg² only): 1 non-temporal, 2 cached, 0 the size
+// rule; an explicit environment policy wins over it
+inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false, int hint = 0) {
   static const int policy = [] {
     const char* e = std::getenv("GS_NT_READ_ONCE");
     return e ? std::atoi(e) : 2;
@@ -140,7 +142,9 @@ inline bool nt_read_once(int64_t stream_bytes, bool sqnorm = false) {
     return e ? std::atoi(e) : 2;
   }();
   const int pol = sqnorm ? policy_sq : policy;
-  return pol == 2 ? stream_bytes > kInfinityCacheBytes : pol != 0;
+  if (pol != 2) return pol != 0;
+  if (hint == 1 || hint == 2) return hint == 1;
+  return stream_bytes > kInfinityCacheBytes;
 }
 inline int dtype_bytes(int dt) { return dt == GS_F32 ? 4 : 2; }
 // in-kernel combine of chunk-engine reductions (two-level ticket over R groups)

@@ -317,11 +317,12 @@ static int sqnorm_nt(gs_plan* p, int slot, int dt, float* sq, int acc, int group
   });
   return GS_OK;
 }
-// the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once);
+// the slot is read once: non-temporal loads beyond the Infinity Cache (nt_read_once),
+// or as the caller's hint says (who wrote the grads: gs_plan_set_read_hint);
 // a non-temporal Σg² leaves the grads out of the caches, so the update that
 // follows loads them non-temporally too (grads_read cleared)
 static int sqnorm_launch(gs_plan* p, int slot, int dt, float* sq, int acc, int groups_only, void* stream) {
-  if (!nt_read_once(p->elems * dtype_bytes(dt), true))
+  if (!nt_read_once(p->elems * dtype_bytes(dt), true, p->read_hint))
     return sqnorm_nt<false>(p, slot, dt, sq, acc, groups_only, stream);
   p->grads_read = false;
   return sqnorm_nt<true>(p, slot, dt, sq, acc, groups_only, stream);

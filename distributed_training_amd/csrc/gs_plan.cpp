@@ -372,6 +372,13 @@ int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, in
   return hip_sqnorm_partial(p, slot, dtype, groups_out, n_groups, stream);
 }
 
+int gs_plan_set_read_hint(gs_plan* p, int hint) {
+  PLAN_OK(p);
+  GS_CHECK_ARG(hint >= 0 && hint <= 2, "gs_plan_set_read_hint: hint 0, 1 or 2");
+  p->read_hint = hint;
+  return GS_OK;
+}
+
 int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
                      float coef_mul, float* out_dev) {
   PLAN_OK(p);

@@ -198,6 +198,11 @@ class TensorListPlan:
                                                 None if out is None else out.data_ptr()), "gs_plan_set_clip_groups")
         self._clip_refs = (groups, out)
 
+    def set_read_hint(self, hint: int):
+        """How this plan's Σg² kernels load their slot (gs_plan_set_read_hint): 0 the
+        size rule, 1 non-temporal, 2 cached."""
+        L.check(L.lib().gs_plan_set_read_hint(self.handle, int(hint)), "gs_plan_set_read_hint")
+
     def set_clip(self, max_norm: float | None, eps: float = 1e-6, sqnorm: torch.Tensor | None = None,
                  sq_mul: float = 1.0, coef_mul: float = 1.0, out: torch.Tensor | None = None):
         """Fold the clip coefficient min(1, max_norm/(‖g‖+eps)) into the later

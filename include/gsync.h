@@ -232,6 +232,14 @@ int gs_sqnorm_partial(gs_plan* p, int slot, int dtype, void* stream);
  * (ZeRO: (1/scale)², 1/scale), 1 = none.
  * replaces: T:nn/utils/clip_grad.py:165-174 (clip_coef, clamp, _foreach_mul_)
  *           DeepSpeed gradient_clipping (R:resnet/deepspeed/deepspeed_train.py:195) */
+/* How the plan's Σg² kernels (gs_sqnorm, gs_sqnorm_partial, gs_sqnorm_partial_out)
+ * load their slot: 0 (default) cached below the 256 MiB Infinity Cache and
+ * non-temporal above it; 1 non-temporal (the grads were just written by
+ * non-temporal stores — libgsync's unpack — or by backward, and are read once);
+ * 2 cached (e.g. a shard RCCL's reduce-scatter just wrote).  Bits never change.
+ * GS_NT_SQNORM in the environment overrides.  No reference counterpart (a load
+ * policy of this implementation). */
+int gs_plan_set_read_hint(gs_plan* p, int hint);
 int gs_plan_set_clip(gs_plan* p, const float* sqnorm_dev, float max_norm, float eps, float sq_mul,
                      float coef_mul, float* out_dev);
 /* The partial sums of Σx² over the plan, written out for a sharded optimizer:
