@@ -459,6 +459,45 @@ def test_nt_read_once_policy_changes_no_bits_gpu():
     assert res[0] == res[1] == res[2], res
 
 
+def test_read_hint_setter_cpu():
+    """gs_plan_set_read_hint takes 0 / 1 / 2 (a host plan keeps it and ignores it)."""
+    plan = D.multi_tensor.TensorListPlan([1000, 7], torch.device("cpu"))
+    for h in (1, 2, 0):
+        plan.set_read_hint(h)
+    with pytest.raises(D._lib.GsyncError, match="hint"):
+        plan.set_read_hint(3)
+
+
+@pytest.mark.gpu
+def test_read_hint_changes_no_bits_gpu():
+    """Σg², its group sums and its raw partials (a small plan) below the cache size
+    give the same bits with the default rule (cached there), the non-temporal hint
+    and the cached hint: the hint moves the bytes differently, never the order."""
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(21)
+    sizes = [2048 * 1000, 1000, 512 * 2048, 64 * 3 * 49, 7, 2048 * 4096]
+    xs = [torch.randn(k, device=dev, generator=gen) * 0.01 for k in sizes]
+    small = (torch.randn(3194688, device=dev, generator=gen) * 1e-3).to(torch.bfloat16)
+    res = []
+    for h in (0, 1, 2):
+        plan = D.multi_tensor.TensorListPlan(sizes, dev)
+        plan.set_ptrs(1, xs)
+        plan.set_read_hint(h)
+        sq = torch.zeros(1, device=dev)
+        plan.sqnorm(1, torch.float32, sq)
+        gr = torch.zeros(D._lib.GS_RED_PARTIALS, device=dev)
+        plan.sqnorm_partial_out(1, torch.float32, gr)
+        sp = D.multi_tensor.TensorListPlan([small.numel()], dev)
+        sp.set_ptrs(1, [small])
+        sp.set_read_hint(h)
+        gs = torch.zeros(D._lib.GS_RED_PARTIALS, device=dev)
+        sp.sqnorm_partial_out(1, torch.bfloat16, gs)
+        torch.cuda.synchronize()
+        res.append((sq.cpu(), gr.cpu(), gs.cpu()))
+    for r in res[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(res[0], r))
+
+
 def _ddp_fused_norm(rank, ws, device="cpu", steps=4):
     """FusedSGD.fuse_grad_norm_into(ddp): Σg² of the averaged grads formed inside
     the DDP's bucket unpacks (several buckets, accumulated in bucket order), the
