@@ -148,6 +148,7 @@ def _check_line(d, n):
     # every grad-sync kernel alone on the model's params (the north star's >= 70 % covers them all)
     k = d["grad_sync_kernels"]
     assert set(k["kernels"]) == {"pack_f32", "pack_f32_to_bf16", "unpack_f32", "unpack_f32+sqnorm", "sqnorm_f32",
+                                 "sqnorm_f32_after_unpack", "sqnorm_f32_after_unpack_nt",
                                  "pack_bf16", "unpack_bf16_to_f32", "sgd_momentum_wd", "sqnorm_partial_f32",
                                  "clip_path_sgd", "adam"}
     # the folded clip path: Σg² partials + the clipped update, both launches in one row
