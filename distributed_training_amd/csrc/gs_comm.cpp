@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <algorithm>
 #include <chrono>
 #include <deque>
 #include <functional>
@@ -158,16 +159,24 @@ void watchdog_loop(gs_comm* c) {
       abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       continue;
     }
-    while (!c->inflight.empty() && hipEventQuery(c->inflight.front().ev) == hipSuccess) {
-      if (c->inflight.front().pooled) c->ev_pool.push_back(c->inflight.front().ev);
-      c->inflight.pop_front();
+    // every completed entry leaves, wherever it sits (a caller's event is re-recorded
+    // each step: it may stay pending while later entries complete), and the oldest
+    // pending one is the one timed
+    int64_t oldest_ms = -1;
+    const auto now = clk::now();
+    for (auto it = c->inflight.begin(); it != c->inflight.end();) {
+      if (hipEventQuery(it->ev) == hipSuccess) {
+        if (it->pooled) c->ev_pool.push_back(it->ev);
+        it = c->inflight.erase(it);
+      } else {
+        oldest_ms = std::max<int64_t>(oldest_ms,
+                                      std::chrono::duration_cast<std::chrono::milliseconds>(now - it->t0).count());
+        ++it;
+      }
     }
-    if (!c->inflight.empty() && c->timeout_ms > 0) {
-      const auto age = std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - c->inflight.front().t0);
-      if (age.count() > c->timeout_ms)
-        abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age.count()) +
-                            " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
-    }
+    if (oldest_ms > c->timeout_ms && c->timeout_ms > 0)
+      abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(oldest_ms) +
+                          " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
   }
 }
 
@@ -204,11 +213,21 @@ int comm_track_locked(gs_comm* c, hipStream_t stream) {
 // packet sits between a collective and its unpack (~4.7 µs of stream time each,
 // scripts/micro/event_chain.hip).  The caller keeps the event
 // and calls comm_forget_event before destroying it.
+// The caller's events are re-recorded every step (a bucket's mark): one entry per
+// event, whose clock restarts at each new record — a record supersedes the one
+// before it (hipEventQuery reports the latest), and a hung collective stops the
+// stream, so the entry then ages past the timeout as the host stalls behind it.
 int comm_track_event(gs_comm* c, hipEvent_t ev) {
   if (!c || !ev) return GS_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->timeout_ms <= 0) return GS_OK;
-  c->inflight.push_back({ev, std::chrono::steady_clock::now(), false});
+  const auto now = std::chrono::steady_clock::now();
+  for (auto& f : c->inflight)
+    if (!f.pooled && f.ev == ev) {
+      f.t0 = now;
+      return GS_OK;
+    }
+  c->inflight.push_back({ev, now, false});
   return GS_OK;
 }
 

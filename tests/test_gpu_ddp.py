@@ -461,8 +461,9 @@ def test_communicator_watchdog_and_abort(cuda_device):
 def test_ddp_watchdog_marks_on_unpacks(cuda_device, rccl_pg):
     """The bucketer hands each collective to the RCCL watchdog through the stop
     event its unpack kernel carries (no event packet after the collective): with
-    a 400 ms timeout, steps at timeline levels 0, 1 and 2 complete, and after a
-    wait longer than the timeout nothing counts as hung; closing the DDP drops
+    a 400 ms timeout, steps queued back to back at timeline levels 0, 1 and 2
+    (each bucket's mark re-recorded before its last record completed) complete,
+    and after a wait longer than the timeout nothing counts as hung; closing the DDP drops
     the bucketer's events from the watchdog; the grads equal the hooks' own at
     world size 1."""
     import time
@@ -480,10 +481,14 @@ def test_ddp_watchdog_marks_on_unpacks(cuda_device, rccl_pg):
     saved = comm.timeout_ms
     comm.set_timeout(400)
     g = torch.Generator(device=cuda_device).manual_seed(3)
+    x = torch.rand(8, 3, 32, 32, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=cuda_device, generator=g)
     for level in (0, 1, 2, 1):
         ddp.set_timeline(level)
-        x = torch.rand(8, 3, 32, 32, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
-        y = torch.randint(0, 10, (8,), device=cuda_device, generator=g)
+        # steps queued back to back (the host ahead of the GPU re-records each bucket's
+        # mark before the last record completed), then one checked step
+        for _ in range(8):
+            torch.nn.functional.cross_entropy(ddp(x), y).backward()
         for p in params:
             p.grad = None
         torch.nn.functional.cross_entropy(ddp(x), y).backward()
