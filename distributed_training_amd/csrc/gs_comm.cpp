@@ -159,24 +159,39 @@ void watchdog_loop(gs_comm* c) {
       abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       continue;
     }
-    // every completed entry leaves, wherever it sits (a caller's event is re-recorded
-    // each step: it may stay pending while later entries complete), and the oldest
-    // pending one is the one timed
-    int64_t oldest_ms = -1;
+    // Completed entries leave wherever they sit (a caller's event is re-recorded each
+    // step: it may stay pending while later entries complete).  The lock is held for
+    // a few event queries per poll, not one per entry: an enqueue waiting on it (the
+    // exposed tail's collective at the end of backward) would wait for them.  Every
+    // entry past the timeout is queried; of the others, kQueries per poll.
+    // A queried entry still pending moves to the back, so the queries rotate
+    // through the list.
+    constexpr int kQueries = 4;
+    int budget = kQueries;
     const auto now = clk::now();
+    std::vector<gs_comm::Inflight> requeue;
     for (auto it = c->inflight.begin(); it != c->inflight.end();) {
+      const int64_t age = std::chrono::duration_cast<std::chrono::milliseconds>(now - it->t0).count();
+      const bool overdue = c->timeout_ms > 0 && age > c->timeout_ms;
+      if (!overdue && budget <= 0) {
+        ++it;
+        continue;
+      }
+      if (!overdue) --budget;
       if (hipEventQuery(it->ev) == hipSuccess) {
         if (it->pooled) c->ev_pool.push_back(it->ev);
         it = c->inflight.erase(it);
-      } else {
-        oldest_ms = std::max<int64_t>(oldest_ms,
-                                      std::chrono::duration_cast<std::chrono::milliseconds>(now - it->t0).count());
-        ++it;
+        continue;
       }
+      if (overdue) {
+        abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age) + " ms (timeout " +
+                            std::to_string(c->timeout_ms) + " ms); communicator aborted");
+        break;
+      }
+      requeue.push_back(*it);
+      it = c->inflight.erase(it);
     }
-    if (oldest_ms > c->timeout_ms && c->timeout_ms > 0)
-      abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(oldest_ms) +
-                          " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
+    for (const gs_comm::Inflight& f : requeue) c->inflight.push_back(f);
   }
 }
 
