@@ -5,7 +5,7 @@
 # trace of the end of backward (scripts/tail_trace.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r5t; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-r5t}; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_gpu_comm_api.py tests/test_gpu_one_comm.py tests/test_gpu_ddp.py tests/test_gpu_native_hook.py tests/test_gpu_comm_hooks.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; tail -n 3 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
