@@ -131,6 +131,10 @@ def parse():
                     help="after the timed region: re-wrap the model with each DDP bucket policy (torch, xgmi, "
                          "last-bucket cap 1 MiB, torch again) and time each, with tail, bus bandwidth and parity "
                          "(-1: only at N > 1 on the DDP engine) — the data for DESIGN §8's policy rule")
+    ap.add_argument("--torch-leg", type=int, default=-1,
+                    help="after the legs: the reference's own GPU path (torch DDP + torch.optim.SGD foreach) on the "
+                         "same model / batch / step, timed like the headline; vs_baseline = libgsync / it "
+                         "(-1: only at N = 1)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -510,10 +514,15 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
 # the update rows' mixes as scripts/micro/stream_mix.hip names its plain-stream cases
 LIVE_MIX_CASES = {"sgd3r2w": ("sgd3r2w_g2", "sgd3r2w_g4", "sgd3r2w_g4_ntl"),
                   "adam4r3w": ("adam4r3w_g4", "adam4r3w_g4_ntl"),
-                  "copy": ("copy_g4", "copy_g4_ntl"), "read": ("read_sum_g4", "read_sum_g4_ntl")}
-# the beyond-cache rows whose stream mix one of them is exactly (fp32 throughout)
+                  "copy": ("copy_g4", "copy_g4_ntl"), "read": ("read_sum_g4", "read_sum_g4_ntl"),
+                  # the 16-bit rows: bf16 -> bf16 (4 B/elem), fp32 -> bf16 and bf16 -> fp32 (6 B/elem)
+                  "cvt16_16": ("cvt16_16_e4", "cvt16_16_e8", "cvt16_16_e8_ntl"),
+                  "cvt32_16": ("cvt32_16_e4", "cvt32_16_e8", "cvt32_16_e4_ntl"),
+                  "cvt16_32": ("cvt16_32_e4", "cvt16_32_e8", "cvt16_32_e8_ntl")}
+# the beyond-cache rows whose stream mix one of them is exactly
 LIVE_MIX_OF_ROW = {"sgd_momentum_wd": "sgd3r2w", "adam": "adam4r3w", "pack_f32": "copy", "unpack_f32": "copy",
-                   "sqnorm_f32": "read", "sqnorm_partial_f32": "read"}
+                   "sqnorm_f32": "read", "sqnorm_partial_f32": "read", "pack_bf16": "cvt16_16",
+                   "pack_f32_to_bf16": "cvt32_16", "unpack_bf16_to_f32": "cvt16_32"}
 
 
 def _live_mix_ceiling(dev):
@@ -596,15 +605,37 @@ def _engine_comm(ddp, zero):
 
 
 # Cost estimates of the optional legs after the timed region (seconds), for the
-# --wall-budget-s skip decision: the larger of the N=1 runs with every leg on
-# (profiles/r3/r3n_bench_n1_all_legs.json; profiles/r5/r5a_bench_legs_n1.json: zero2
-# 1.2 s, colossal 35.3 s) and the 4-rank full-size rehearsals
-# (profiles/r3/rehearsal/n4_gloo_r50_full_all_legs_final.json,
-# profiles/r4/r4d_n4_budget240.json), doubled, and at least 5 s; zero2 / colossal
-# include their first-step MIOpen compiles; the policy A/B has 8 variants since r5.
+# --wall-budget-s skip decision.  LEG_COST_S is the one-GPU figure: the larger of the
+# N=1 runs with every leg on (profiles/r3/r3n_bench_n1_all_legs.json;
+# profiles/r5/r5a_bench_legs_n1.json: zero2 1.2 s, colossal 35.3 s) and the 4-rank
+# full-size rehearsals divided by their 4 ranks' share of the one GPU
+# (profiles/r4/r4d_n4_budget240.json), doubled, at least 5 s; zero2 / colossal include
+# their first-step MIOpen compiles; the policy A/B has 8 variants since r5.  leg_cost()
+# scales it with the world size:
+#   * nccl (one rank per GPU): the ranks' GPU work runs in parallel, so the base holds;
+#     what grows with N is each collective's latency and communicator set-up (the A/B's
+#     rccl_max_ctas variant and the xgmi calibration bring up / time their own) and the
+#     concurrent first-step MIOpen compiles of N processes on the node's host cores:
+#     LEG_GROWTH_PER_RANK of the base per extra rank, plus LEG_FIXED_PER_RANK_S for the
+#     legs that create communicators;
+#   * gloo (the rehearsal: N ranks share the box's GPUs): every rank's GPU work
+#     serialises on the shared device — the base times the ranks per GPU — plus the same
+#     per-rank growth.
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
-              "zero2": 2 * 2 * 18.4,  # at N > 1 two engines (default + overlap_allgather)
-              "colossal": 2 * 63.6, "bucket_policy_ab": 2 * 35.0 * 8 / 6}
+              "zero2": 2 * 2 * 18.4 / 4,  # at N > 1 two engines (default + overlap_allgather)
+              "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0}
+LEG_GROWTH_PER_RANK = 0.10
+LEG_FIXED_PER_RANK_S = {"bucket_policy_ab": 1.0, "zero2": 0.25, "colossal": 0.25, "collective_bench": 0.25}
+
+
+def leg_cost(name, world, backend, ranks_per_gpu=1):
+    """Estimated seconds of leg `name` at `world` ranks (see LEG_COST_S)."""
+    base = LEG_COST_S.get(name, 5.0)
+    share = max(1, ranks_per_gpu) if backend == "gloo" else 1
+    return max(5.0, base * share * (1.0 + LEG_GROWTH_PER_RANK * (world - 1))
+               + LEG_FIXED_PER_RANK_S.get(name, 0.0) * (world - 1))
+
+
 # the reference's DeepSpeed optimizer (R:resnet/deepspeed/deepspeed_train.py:175-186): "Adam" in
 # AdamW mode, betas (0.8, 0.999), eps 1e-8, weight_decay 3e-7; gradient_clipping 1.0 (:195)
 DS_ADAM = dict(lr=1e-3, betas=(0.8, 0.999), eps=1e-8, weight_decay=3e-7)
@@ -875,6 +906,53 @@ def colossal_leg(args, world, rank, dev, coll_h, batch=128, steps=8, warmup=8):
     opt_w.zero_grad()
     ddp.close()
     del cmodel, opt_w, ddp, model
+    torch.cuda.empty_cache()
+    return out
+
+
+def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
+    """The reference's own GPU path beside the headline, in the same run (VERDICT r5
+    next 5): a fresh model of the same architecture and seed, torch's
+    DistributedDataParallel over the nccl (RCCL) process group, bf16 autocast,
+    torch.optim.SGD(lr 0.1, momentum 0.9, wd 1e-4, foreach) — the headline's step with
+    torch's Reducer and foreach optimizer in place of libgsync
+    (R:resnet/pytorch_ddp/ddp_train.py:95-97 wraps the model in DDP and steps a
+    torch.optim optimizer) — `steps` timed steps bracketed like the headline's."""
+    from distributed_training_amd.resnet import MODELS
+
+    torch.manual_seed(0)
+    model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=mf)
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], bucket_cap_mb=args.bucket_cap_mb)
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=True)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=mf)
+    y = torch.randint(0, 1000, (args.batch,), device=dev, generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def one():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = crit(ddp(x), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    out = {"impl": "torch DistributedDataParallel + torch.optim.SGD(foreach), bf16 autocast, channels_last",
+           "images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+           "warmup": warmup, "per_gpu_batch": args.batch,
+           "timing": "barrier + synchronize on both sides, MAX over ranks (as the headline)"}
+    del ddp, opt, model
     torch.cuda.empty_cache()
     return out
 
@@ -1362,6 +1440,17 @@ def main():
             line["leg_errors"] = dict(leg_errors)
         if leg_seconds:
             line["leg_seconds"] = dict(leg_seconds)
+            line["leg_estimates_s"] = dict(leg_estimates, model="leg_cost(): LEG_COST_S x (ranks per GPU under gloo) "
+                                                               f"x (1 + {LEG_GROWTH_PER_RANK} (N-1)) + per-rank "
+                                                               "communicator set-up")
+        if torch_ddp is not None:
+            line["torch_ddp"] = torch_ddp
+            if torch_ddp.get("images_per_sec"):
+                line["vs_baseline"] = img_s / torch_ddp["images_per_sec"]
+                line["vs_baseline_basis"] = (
+                    "the reference's own GPU path timed in this run: torch DistributedDataParallel + "
+                    "torch.optim.SGD(foreach) on the same model, batch, data and step "
+                    "(R:resnet/pytorch_ddp/ddp_train.py:95-97); BASELINE.md publishes no number")
         return line
 
     # ---- after the timed region.  The headline is complete here; what follows are
@@ -1375,20 +1464,25 @@ def main():
     # budget ends (a hung collective) gets a watchdog that prints the line with the
     # legs completed so far and ends every rank with exit status 3.
     tail = timeline = tail_timed = None
-    coll = kernel_rates = parity = policy_ab = zero2 = colossal = None
+    coll = kernel_rates = parity = policy_ab = zero2 = colossal = torch_ddp = None
     leg_errors: dict = {}
     current_leg = ["start"]
 
     leg_seconds: dict = {}
     budget = args.wall_budget_s
 
+    ranks_per_gpu = -(-world // max(1, torch.cuda.device_count()))
+    leg_estimates: dict = {}
+
     def fits(name):
+        est = leg_cost(name, world, args.pg_backend, ranks_per_gpu)
+        leg_estimates[name] = round(est, 1)
         if budget <= 0:
             return True
         left = budget - coll_h.max(time.time() - T_START)
-        if LEG_COST_S.get(name, 5.0) <= left:
+        if est <= left:
             return True
-        leg_errors[name] = (f"skipped: estimated {LEG_COST_S.get(name, 5.0):.0f} s > {max(left, 0.0):.0f} s left "
+        leg_errors[name] = (f"skipped: estimated {est:.0f} s > {max(left, 0.0):.0f} s left "
                             f"of --wall-budget-s {budget:.0f}")
         if rank == 0:
             print(f"[bench] leg {name} {leg_errors[name]}", file=sys.stderr, flush=True)
@@ -1506,6 +1600,13 @@ def main():
         if rank == 0 and colossal is not None:
             print(f"[bench] colossal leg: {colossal['images_per_sec']:.1f} images/s, "
                   f"parity {colossal['parity'].get('ok')}", file=sys.stderr, flush=True)
+    want_torch = args.torch_leg == 1 or (args.torch_leg == -1 and world == 1)
+    if (want_torch and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
+            and args.pg_backend == "nccl"):
+        torch_ddp = leg("torch_ddp", lambda: torch_ddp_leg(args, world, rank, dev, mf))
+        if rank == 0 and torch_ddp is not None:
+            print(f"[bench] torch DDP leg: {torch_ddp['images_per_sec']:.1f} images/s "
+                  f"(libgsync {img_s:.1f})", file=sys.stderr, flush=True)
     want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
     if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
             and not args.optimizer_overlap):
@@ -1516,6 +1617,17 @@ def main():
     current_leg[0] = "done"
     if watchdog is not None:
         watchdog.cancel()
+    # tear down what the run created before the process group goes, as the reference
+    # does (R:resnet/pytorch_ddp/ddp_train.py:87-88,105): the engines, then libgsync's
+    # communicators
+    if args.impl == "libgsync":
+        for eng in (zero, ddp, getattr(ddp, "module", None)):
+            if isinstance(eng, (D.DistributedDataParallel,)) or type(eng).__name__ == "ZeroDataParallel":
+                try:
+                    eng.close()
+                except Exception as ex:  # the line still prints
+                    print(f"[bench] close: {ex!r}", file=sys.stderr, flush=True)
+        D.destroy_communicators()
 
     # free the engines (reference cycles hold the process group) before the teardown:
     # a gloo worker thread dropping a Python tensor during interpreter finalization

@@ -9,7 +9,7 @@ Public surface:
   compat.deepspeed / compat.colossalai   API shims for the other two trainers
 """
 from . import _lib  # noqa: F401
-from .comm import Communicator, get_communicator  # noqa: F401
+from .comm import Communicator, destroy_communicators, get_communicator  # noqa: F401
 from .ddp import DDP, DistributedDataParallel, GradBucket, compute_bucket_assignment_by_size  # noqa: F401
 from .graphs import CapturedStep  # noqa: F401
 from .flatten import copy_flat_to, flatten_dense_tensors, unflatten_dense_tensors  # noqa: F401

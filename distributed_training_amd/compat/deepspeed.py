@@ -320,6 +320,10 @@ class DeepSpeedEngine(nn.Module):
         tag = f"global_step{self.global_steps}" if tag is None else str(tag)
         path = os.path.join(save_dir, tag)
         rank = self.global_rank
+        if self._zero is not None:
+            # overlap_allgather: the last step's parameter all-gathers may still run on the
+            # communicator's stream; the module state read below must follow them
+            self._zero.wait_allgather()
         if rank == 0:
             os.makedirs(path, exist_ok=True)
         dist.barrier()
@@ -349,6 +353,8 @@ class DeepSpeedEngine(nn.Module):
             with open(latest) as f:
                 tag = f.read().strip()
         path = os.path.join(load_dir, str(tag))
+        if self._zero is not None:
+            self._zero.wait_allgather()  # a pending all-gather must not land on the loaded parameters
         ms = torch.load(os.path.join(path, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
         if ms["dp_world_size"] != self.world_size and self._zero is not None:
             raise RuntimeError(f"checkpoint has {ms['dp_world_size']} ZeRO shards, this job {self.world_size}")
@@ -370,7 +376,7 @@ class DeepSpeedEngine(nn.Module):
     def consolidated_fp32_state_dict(self):
         """zero_to_fp32: the full fp32 model state_dict (collective under ZeRO)."""
         if self._zero is not None:
-            return self._zero.consolidated_state_dict()
+            return self._zero.consolidated_state_dict()  # waits for pending all-gathers itself
         return {k: v.detach().float().cpu() if v.is_floating_point() else v.detach().cpu()
                 for k, v in self.module.state_dict().items()}
 

@@ -47,6 +47,8 @@ namespace {
       return fail(GS_EHIP, std::string(#expr " failed: ") + hipGetErrorString(_e));  \
   } while (0)
 
+constexpr int kWdRing = 8;
+
 struct Bucket {
   std::vector<int32_t> params;  // global parameter ids, bucket order
   gs_plan* plan = nullptr;      // layout of the params inside the flat bucket
@@ -63,7 +65,11 @@ struct Bucket {
   // ready -> pk0 (queue) -> t0 (pack) -> t1 (collective) -> u1 (unpack)
   hipEvent_t ev_ready = nullptr, ev_pk0 = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_u1 = nullptr;
   hipEvent_t ev_sync = nullptr;  // untimed ready event (a comm-stream chain waits on it)
-  hipEvent_t ev_wd = nullptr;    // the watchdog's mark of the collective, carried by the unpack kernel
+  // the watchdog's marks of the collective, carried by the unpack kernel: a ring, so a
+  // host queueing steps ahead re-records an event only after its previous record
+  // completed (comm_track_event); timing-enabled, as the level-1 tail's done mark
+  hipEvent_t ev_wd[kWdRing] = {};
+  int wd_next = 0;
   bool timed = false;            // pk0 / t0 / t1 / u1 recorded (level 2)
   bool pk0_is_ready = false;     // the producer-side tail: its pack follows the ready mark on the same
                                  // stream with nothing between, so ready doubles as pk0 (queue 0)
@@ -312,8 +318,20 @@ int launch_bucket(gs_bucketer* b, int bi) {
     // after the collective: a packet costs ~4.7 µs of stream time, a kernel-carried
     // stop ~2.4 (scripts/micro/event_chain.hip) — the whole gap between the tail's
     // pack and unpack at N = 1 (scripts/tail_trace.py)
+    // The event stands for one record (comm_track_event): the ring's next slot, or u1
+    // at level 2, only once its previous record completed — a host that runs a whole
+    // ring of steps ahead of the GPU gets a pooled packet after the collective instead.
+    // At level 1 the producer-side tail's slot is also this step's done mark.
     const bool unpacks = b->do_unpack() || b->found_inf;
-    hipEvent_t wd_ev = (!capturing && unpacks && comm_watching(b->comm)) ? (end_ev ? end_ev : bk.ev_wd) : nullptr;
+    hipEvent_t wd_ev = nullptr;
+    if (!capturing && unpacks && comm_watching(b->comm)) {
+      hipEvent_t cand = timed ? bk.ev_u1 : bk.ev_wd[bk.wd_next];
+      if (hipEventQuery(cand) == hipSuccess) {
+        wd_ev = cand;
+        if (!timed) bk.wd_next = (bk.wd_next + 1) % kWdRing;
+        if (chain_end) end_ev = b->done_ev = wd_ev;
+      }
+    }
     GS_TRY_RET(launch_collective(b, bk, cs, wd_ev == nullptr));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
     // unpack: t1 a packet before it, its stop = u1 or the done mark; the collective lies
@@ -417,9 +435,10 @@ int gs_bucketer_create(gs_comm* comm, int device_kind, int device, int n_params,
       if (hipEventCreate(&bk.ev_ready) != hipSuccess || hipEventCreate(&bk.ev_pk0) != hipSuccess ||
           hipEventCreate(&bk.ev_t0) != hipSuccess || hipEventCreate(&bk.ev_t1) != hipSuccess ||
           hipEventCreate(&bk.ev_u1) != hipSuccess ||
-          hipEventCreateWithFlags(&bk.ev_sync, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&bk.ev_wd, hipEventDisableTiming) != hipSuccess)
+          hipEventCreateWithFlags(&bk.ev_sync, hipEventDisableTiming) != hipSuccess)
         return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
+      for (hipEvent_t& ev : bk.ev_wd)
+        if (hipEventCreate(&ev) != hipSuccess) return bail(fail(GS_EHIP, "gs_bucketer_create: event creation failed"));
     }
   }
   for (int p = 0; p < n_params; ++p)
@@ -441,13 +460,15 @@ int gs_bucketer_destroy(gs_bucketer* b) {
     comm_forget_event(b->comm, b->ev_done);
     for (Bucket& bk : b->buckets) {
       comm_forget_event(b->comm, bk.ev_u1);
-      comm_forget_event(b->comm, bk.ev_wd);
+      for (hipEvent_t ev : bk.ev_wd) comm_forget_event(b->comm, ev);
     }
   }
   for (Bucket& bk : b->buckets) {
     gs_plan_destroy(bk.plan);
     gs_plan_destroy(bk.flat);
-    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1, bk.ev_sync, bk.ev_wd})
+    for (hipEvent_t ev : {bk.ev_ready, bk.ev_pk0, bk.ev_t0, bk.ev_t1, bk.ev_u1, bk.ev_sync})
+      if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : bk.ev_wd)
       if (ev) (void)hipEventDestroy(ev);
   }
   if (b->ev_done) (void)hipEventDestroy(b->ev_done);

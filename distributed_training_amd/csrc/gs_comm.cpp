@@ -46,9 +46,14 @@ struct gs_comm {
   struct Inflight {
     hipEvent_t ev;
     std::chrono::steady_clock::time_point t0;
-    bool pooled;  // from ev_pool (a packet after the collective) or the caller's (comm_track_event)
   };
-  std::deque<Inflight> inflight;
+  // packets recorded after a collective (comm_track_locked), in enqueue order: retired
+  // from the front, so each poll queries the entries it retires and one pending one
+  std::deque<Inflight> pooled;
+  // the callers' own events (comm_track_event: the bucketer's unpack-carried marks), one
+  // entry per event, each standing for one record; a few of them are queried per poll
+  std::vector<Inflight> caller;
+  size_t caller_next = 0;  // rotation cursor over `caller`
   std::vector<hipEvent_t> ev_pool;
 };
 
@@ -159,39 +164,61 @@ void watchdog_loop(gs_comm* c) {
       abort_locked(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       continue;
     }
-    // Completed entries leave wherever they sit (a caller's event is re-recorded each
-    // step: it may stay pending while later entries complete).  The lock is held for
-    // a few event queries per poll, not one per entry: an enqueue waiting on it (the
-    // exposed tail's collective at the end of backward) would wait for them.  Every
-    // entry past the timeout is queried; of the others, kQueries per poll.
-    // A queried entry still pending moves to the back, so the queries rotate
-    // through the list.
-    constexpr int kQueries = 4;
-    int budget = kQueries;
+    // Pooled packets: retired from the front while complete (at most kRetire a poll, so
+    // the lock is never held for a long backlog), the front's age decides a timeout —
+    // every later packet was enqueued after it.  The lock is held for the queries of
+    // one poll: an enqueue waiting on it (the exposed tail's collective at the end of
+    // backward) waits for them.
+    constexpr int kRetire = 64;
     const auto now = clk::now();
-    std::vector<gs_comm::Inflight> requeue;
-    for (auto it = c->inflight.begin(); it != c->inflight.end();) {
-      const int64_t age = std::chrono::duration_cast<std::chrono::milliseconds>(now - it->t0).count();
-      const bool overdue = c->timeout_ms > 0 && age > c->timeout_ms;
-      if (!overdue && budget <= 0) {
-        ++it;
-        continue;
-      }
-      if (!overdue) --budget;
-      if (hipEventQuery(it->ev) == hipSuccess) {
-        if (it->pooled) c->ev_pool.push_back(it->ev);
-        it = c->inflight.erase(it);
-        continue;
-      }
-      if (overdue) {
-        abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age) + " ms (timeout " +
-                            std::to_string(c->timeout_ms) + " ms); communicator aborted");
+    auto age_ms = [&](const gs_comm::Inflight& f) {
+      return std::chrono::duration_cast<std::chrono::milliseconds>(now - f.t0).count();
+    };
+    bool front_pending = false;
+    for (int n = 0; n < kRetire && !c->pooled.empty(); ++n) {
+      const gs_comm::Inflight& f = c->pooled.front();
+      if (hipEventQuery(f.ev) != hipSuccess) {
+        front_pending = true;
         break;
       }
-      requeue.push_back(*it);
-      it = c->inflight.erase(it);
+      c->ev_pool.push_back(f.ev);
+      c->pooled.pop_front();
     }
-    for (const gs_comm::Inflight& f : requeue) c->inflight.push_back(f);
+    if (front_pending && c->timeout_ms > 0 && age_ms(c->pooled.front()) > c->timeout_ms) {
+      abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age_ms(c->pooled.front())) +
+                          " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
+      continue;
+    }
+    // The callers' events: every entry past the timeout is queried, of the others
+    // kQueries a poll in rotation; a completed entry leaves the list.
+    constexpr size_t kQueries = 4;
+    const size_t n = c->caller.size();
+    if (n == 0) continue;
+    std::vector<char> done(n, 0);
+    size_t queried = 0;
+    bool aborted = false;
+    for (size_t k = 0; k < n; ++k) {
+      const size_t i = (c->caller_next + k) % n;
+      const gs_comm::Inflight& f = c->caller[i];
+      const int64_t age = age_ms(f);
+      const bool overdue = c->timeout_ms > 0 && age > c->timeout_ms;
+      if (!overdue && queried >= kQueries) continue;
+      if (!overdue) ++queried;
+      if (hipEventQuery(f.ev) == hipSuccess) {
+        done[i] = 1;
+      } else if (overdue) {
+        abort_locked(c, "watchdog: a collective has been in flight for " + std::to_string(age) + " ms (timeout " +
+                            std::to_string(c->timeout_ms) + " ms); communicator aborted");
+        aborted = true;
+        break;
+      }
+    }
+    if (aborted) continue;
+    size_t w = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (!done[i]) c->caller[w++] = c->caller[i];
+    c->caller.resize(w);
+    c->caller_next = w ? (c->caller_next + kQueries) % w : 0;
   }
 }
 
@@ -218,7 +245,7 @@ int comm_track_locked(gs_comm* c, hipStream_t stream) {
     c->ev_pool.push_back(ev);
     return fail(GS_EHIP, "watchdog: event record failed");
   }
-  c->inflight.push_back({ev, std::chrono::steady_clock::now(), true});
+  c->pooled.push_back({ev, std::chrono::steady_clock::now()});
   return GS_OK;
 }
 
@@ -226,23 +253,23 @@ int comm_track_locked(gs_comm* c, hipStream_t stream) {
 // watchdog through an event of the caller's that its stream records after it —
 // the bucketer: each bucket's unpack kernel carries the stop event, so no event
 // packet sits between a collective and its unpack (~4.7 µs of stream time each,
-// scripts/micro/event_chain.hip).  The caller keeps the event
-// and calls comm_forget_event before destroying it.
-// The caller's events are re-recorded every step (a bucket's mark): one entry per
-// event, whose clock restarts at each new record — a record supersedes the one
-// before it (hipEventQuery reports the latest), and a hung collective stops the
-// stream, so the entry then ages past the timeout as the host stalls behind it.
+// scripts/micro/event_chain.hip).  The caller keeps the event and calls
+// comm_forget_event before destroying it.
+// One entry per event, standing for ONE record: the caller re-records an event only
+// after its previous record completed (the bucketer queries it first and rotates
+// through a ring of them, falling back to a pooled packet when the host runs that far
+// ahead), so restarting the entry's clock here never hides a pending collective.
 int comm_track_event(gs_comm* c, hipEvent_t ev) {
   if (!c || !ev) return GS_OK;
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->timeout_ms <= 0) return GS_OK;
   const auto now = std::chrono::steady_clock::now();
-  for (auto& f : c->inflight)
-    if (!f.pooled && f.ev == ev) {
+  for (auto& f : c->caller)
+    if (f.ev == ev) {
       f.t0 = now;
       return GS_OK;
     }
-  c->inflight.push_back({ev, now, false});
+  c->caller.push_back({ev, now});
   return GS_OK;
 }
 
@@ -255,7 +282,9 @@ bool comm_watching(gs_comm* c) {
 void comm_forget_event(gs_comm* c, hipEvent_t ev) {
   if (!c || !ev) return;
   std::lock_guard<std::mutex> lk(c->mu);
-  for (auto it = c->inflight.begin(); it != c->inflight.end();) it = it->ev == ev ? c->inflight.erase(it) : it + 1;
+  c->caller.erase(std::remove_if(c->caller.begin(), c->caller.end(),
+                                 [ev](const gs_comm::Inflight& f) { return f.ev == ev; }),
+                  c->caller.end());
 }
 
 // Enqueue one RCCL collective under c->mu: liveness check, enqueue and
@@ -337,8 +366,7 @@ int gs_comm_destroy(gs_comm* c) {
   }
   (void)hipSetDevice(c->device);
   if (c->stream && !c->aborted.load()) (void)hipStreamSynchronize(c->stream);
-  for (auto& f : c->inflight)
-    if (f.pooled) (void)hipEventDestroy(f.ev);  // the caller's events stay the caller's
+  for (auto& f : c->pooled) (void)hipEventDestroy(f.ev);  // the caller's events stay the caller's
   for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
   if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);

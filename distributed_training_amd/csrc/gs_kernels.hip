@@ -358,6 +358,11 @@ int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t*
       static_cast<int64_t>(p->chunks.size()) <= kRawChunksMax) {
     GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 2, stream));
     if (n_groups) *n_groups = p->red_groups;
+    // the partials live only in the caller's buffer: the plan's own group sums were not
+    // written, so a clip from them (gs_plan_set_clip(sqnorm = NULL)) fails with GS_ESTATE
+    // instead of folding stale or out-of-range slots
+    p->red_valid = false;
+    p->red_groups = 0;
     return GS_OK;
   }
   const int cap = std::min(p->grid_cap, red_grid_cap(SqnormOp<kUnit, GS_F32>::kRedGrid));

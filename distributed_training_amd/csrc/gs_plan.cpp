@@ -426,6 +426,8 @@ static int plan_clip(gs_plan* p, ClipArgs* c, const ClipArgs** out) {
       c->sq = &p->h_red;
       c->groups = 0;
     } else {
+      if (p->red_groups > kRedMaxGroups)
+        return fail(GS_ESTATE, "clipped update from the plan's own Σg²: more group sums than the plan keeps");
       c->groups = p->red_groups;
       c->stride = kRedSyncStride;
       c->sq = p->red_groups > 0 ? hip_plan_red_groups(p) : hip_plan_red_scalar(p);

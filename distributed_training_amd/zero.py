@@ -598,8 +598,11 @@ class ZeroDataParallel:
         if self.lowp:  # the model copy follows the master
             for shard, m in zip(self.param_shards, self.master):
                 shard.copy_(m.to(shard.dtype))
-            for b, flat in enumerate(self.param_flats):
-                self._all_gather_flat(b, flat)
+        # every rank's parameters from the loaded shards (fp32: the master IS this rank's
+        # slice of the flats, the other slices come from the gather, not from whatever the
+        # module held — a module load_state_dict may have run before this)
+        for b, flat in enumerate(self.param_flats):
+            self._all_gather_flat(b, flat)
 
     def _all_gather_flat(self, b, flat):
         shard = flat[self.rank * self.shard_sizes[b]:(self.rank + 1) * self.shard_sizes[b]]
@@ -620,6 +623,7 @@ class ZeroDataParallel:
         (DeepSpeed ``zero_to_fp32`` / ``get_fp32_state_dict_from_zero_checkpoint``;
         Colossal ``save_model(shard=False)``).  Collective: every rank calls it
         and every rank gets it.  Buffers are this rank's."""
+        self.wait_allgather()
         fulls = []
         for b, m in enumerate(self.master):
             full = torch.empty(self.bucket_numel[b], dtype=torch.float32, device=self.device)

@@ -160,6 +160,11 @@ int gs_plan_create(int device_kind, int device, int n_tensors, const int64_t* nu
  * ~1920 tasks, one resident wave of workgroups) */
 int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t* numels,
                       int64_t align_elems, int64_t task_units, gs_plan** out);
+/* Stream lifetime: a plan orders a launch on a new stream after its previous
+ * launch by recording an event on the PREVIOUS launch's stream at that point
+ * (no packet after every launch), and gs_plan_destroy synchronises on it.  So
+ * the stream of a plan's last launch must stay alive until the plan's next
+ * launch on another stream, or until gs_plan_destroy. */
 int gs_plan_destroy(gs_plan* p);
 int64_t gs_plan_flat_numel(gs_plan* p);
 int gs_plan_offsets(gs_plan* p, int64_t* out /* [n_tensors] */);

@@ -10,6 +10,8 @@
 // each (the beyond_ic harness's conditions).  One JSON line per case.  With case
 // names as arguments: only those cases on the one-shot grid, each kernel timed
 // by its own start / stop events (bench.py's live ceiling for the update rows).
+// The cvt* cases are the 16-bit pack / unpack rows' mixes (bf16 -> bf16 4 B/elem,
+// fp32 -> bf16 and bf16 -> fp32 6 B/elem).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -83,6 +85,86 @@ __global__ void __launch_bounds__(256) mix(f4* __restrict__ s0, f4* __restrict__
   }
   if constexpr (W == 0) {
     if (acc == 12345.f) part[blockIdx.x] = acc;  // keeps the loads; never true for zeros
+  }
+}
+
+// The 16-bit rows' mixes (bench.py's pack_bf16, pack_f32_to_bf16, unpack_bf16_to_f32):
+// n elements of IN bytes read from src, converted, n elements of OUT bytes written
+// to dst (non-temporal stores, as copy_*), E elements per lane access (4: libgsync's
+// unit, 8-B bf16 accesses; 8: 16-B bf16 accesses), G accesses in flight per lane.
+// fp32 -> bf16 rounds to nearest even, bf16 -> fp32 is exact.
+template <int E, int IN>
+struct Vec;
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+template <> struct Vec<4, 2> { typedef u2v T; };
+template <> struct Vec<8, 2> { typedef u4v T; };
+template <> struct Vec<4, 4> { typedef u4v T; };
+template <> struct Vec<8, 4> { struct T { u4v a, b; }; };
+
+__device__ __forceinline__ uint32_t bf16_rne(uint32_t u) { return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16; }
+
+template <int E, int IN, bool NT>
+__device__ __forceinline__ void ld_units(const void* p, int64_t i, uint32_t (&w)[E]) {
+  typedef typename Vec<E, IN>::T V;
+  const V* q = reinterpret_cast<const V*>(static_cast<const char*>(p) + i * IN);
+  V v;
+  if constexpr (IN == 4 && E == 8) {
+    v.a = NT ? __builtin_nontemporal_load(&q->a) : q->a;
+    v.b = NT ? __builtin_nontemporal_load(&q->b) : q->b;
+  } else {
+    v = NT ? __builtin_nontemporal_load(q) : *q;
+  }
+  if constexpr (IN == 4) {  // fp32 words
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < E; ++k) w[k] = u[k];
+  } else {  // packed bf16 pairs -> fp32 bit patterns
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < E / 2; ++k) {
+      w[2 * k] = u[k] << 16;
+      w[2 * k + 1] = u[k] & 0xffff0000u;
+    }
+  }
+}
+
+template <int E, int OUT>
+__device__ __forceinline__ void st_units(void* p, int64_t i, const uint32_t (&w)[E]) {
+  typedef typename Vec<E, OUT>::T V;
+  V v;
+  uint32_t* u = reinterpret_cast<uint32_t*>(&v);
+  if constexpr (OUT == 4) {
+#pragma unroll
+    for (int k = 0; k < E; ++k) u[k] = w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < E / 2; ++k) u[k] = bf16_rne(w[2 * k]) | (bf16_rne(w[2 * k + 1]) << 16);
+  }
+  V* q = reinterpret_cast<V*>(static_cast<char*>(p) + i * OUT);
+  if constexpr (OUT == 4 && E == 8) {
+    __builtin_nontemporal_store(v.a, &q->a);
+    __builtin_nontemporal_store(v.b, &q->b);
+  } else {
+    __builtin_nontemporal_store(v, q);
+  }
+}
+
+template <int IN, int OUT, int E, int G, bool NTL>
+__global__ void __launch_bounds__(256) cvt(const void* __restrict__ src, void* __restrict__ dst, int64_t n) {
+  const int64_t step = (int64_t)gridDim.x * 256 * G * E;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * G * E; base < n; base += step) {
+    uint32_t w[G][E];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + ((int64_t)g * 256 + threadIdx.x) * E;
+      if (i < n) ld_units<E, IN, NTL>(src, i, w[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t i = base + ((int64_t)g * 256 + threadIdx.x) * E;
+      if (i < n) st_units<E, OUT>(dst, i, w[g]);
+    }
   }
 }
 
@@ -176,6 +258,29 @@ int main(int argc, char** argv) {
       CASE("sgd3r2w_g2_ntl_streammajor", 20, 3, 2, 2, true, true, true);
       CASE("adam4r3w_g4_ntl_streammajor", 28, 4, 3, 4, true, true, true);
 #undef CASE
+      // 16-bit mixes: src s[0], dst s[1]
+      auto g16 = [&](int E, int G) { return gridc ? gridc : (int)std::min<int64_t>(1 << 30, (n + 256 * G * E - 1) / (256 * G * E)); };
+#define CVT(NAME, BPE, IN, OUT, E, G, NTL)                                                                           \
+  if (wanted(NAME, gridc))                                                                                           \
+  cs.push_back({NAME, BPE,                                                                                           \
+                time_ms([&](hipEvent_t ea, hipEvent_t eb) {                                                          \
+                  if (ea)                                                                                            \
+                    hipExtLaunchKernelGGL((cvt<IN, OUT, E, G, NTL>), dim3(g16(E, G)), dim3(256), 0, 0, ea, eb, 0,    \
+                                          (const void*)s[0], (void*)s[1], n);                                        \
+                  else                                                                                               \
+                    cvt<IN, OUT, E, G, NTL><<<g16(E, G), 256>>>(s[0], s[1], n);                                      \
+                }, 20),                                                                                              \
+                gridc})
+      CVT("cvt16_16_e4", 4, 2, 2, 4, 4, false);
+      CVT("cvt16_16_e8", 4, 2, 2, 8, 4, false);
+      CVT("cvt16_16_e8_ntl", 4, 2, 2, 8, 4, true);
+      CVT("cvt32_16_e4", 6, 4, 2, 4, 4, false);
+      CVT("cvt32_16_e8", 6, 4, 2, 8, 4, false);
+      CVT("cvt32_16_e4_ntl", 6, 4, 2, 4, 4, true);
+      CVT("cvt16_32_e4", 6, 2, 4, 4, 4, false);
+      CVT("cvt16_32_e8", 6, 2, 4, 8, 4, false);
+      CVT("cvt16_32_e8_ntl", 6, 2, 4, 8, 4, true);
+#undef CVT
     }
   }
   for (auto& c : cs) {

@@ -128,7 +128,14 @@ def _check_line(d, n):
         assert k in d, k
     assert d["n_gpus"] == n and d["steps"] == 3 and d["warmup"] == 2
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    if n == 1 and "rehearsal" not in d["config"]:
+        # the reference's own GPU path (torch DDP + torch.optim.SGD foreach) timed in the same run
+        t = d["torch_ddp"]
+        assert t["images_per_sec"] > 0 and t["steps"] > 0 and d["vs_baseline_basis"]
+        assert abs(d["vs_baseline"] - d["value"] / t["images_per_sec"]) <= 1e-9 * d["vs_baseline"]
+    else:
+        assert d["vs_baseline"] is None
     assert d["config"]["workload"] and d["config"]["parallelism"] == f"dp{n}"
     assert d["config"]["global_batch"] == 16 * n
     # value = all ranks' images / the (max-over-ranks) timed region
@@ -169,6 +176,13 @@ def _check_line(d, n):
     assert "error" not in live, live
     assert live["case"].startswith("sgd3r2w") and 0.3 < live["frac"] < 1.0
     assert abs(r["frac_of_live_ceiling"] - r["frac"] / live["frac"]) < 1e-9
+    # every beyond-cache row with an exact plain-stream mix carries its own live ceiling, the
+    # 16-bit pack / unpack rows included
+    lv = b["plain_stream_ceiling_live"]
+    for row, mix in (("pack_bf16", "cvt16_16"), ("pack_f32_to_bf16", "cvt32_16"), ("unpack_bf16_to_f32", "cvt16_32"),
+                     ("pack_f32", "copy"), ("sqnorm_f32", "read")):
+        assert 0.3 < lv[mix]["frac"] < 1.0, (mix, lv.get(mix))
+        assert abs(b["kernels"][row]["frac_of_live_ceiling"] - b["kernels"][row]["frac"] / lv[mix]["frac"]) < 1e-9
     if n == 1:  # configs[3]'s N>1 clip path at its N=8 shard, over the one-rank RCCL communicator
         z, zs = k["clip_path_zero_n8"], k["clip_path_zero_n8_scalar"]
         assert z["alg_bytes"] == 30 * z["shard_elems"] and z["avg_ms"] > 0 and z["kernels_ms"] > 0
