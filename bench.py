@@ -814,6 +814,33 @@ def _zero2_run(args, world, rank, dev, coll_h, steps, warmup, overlap_allgather=
                                                             "run on the communicator's stream under the next "
                                                             "forward" if overlap_allgather else ""))}
     zero.wait_allgather()
+    # the step's end (update + its collectives): HIP events right around zero.step() on
+    # the step's stream, median of 6 untimed steps each, with the collectives' watchdog
+    # marks on the consuming kernels (the default) and with round 5's event packet after
+    # every collective — the same run, the same GPU
+    def step_end_ms(packets):
+        zero.set_mark_packets(packets)
+        evs = []
+        for _ in range(6):
+            zero.prepare_backward()
+            fwd_bwd()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            zero.step()
+            b.record()
+            evs.append((a, b))
+        torch.cuda.synchronize()
+        zero.set_mark_packets(False)
+        return sorted(x.elapsed_time(y) for x, y in evs)[len(evs) // 2]
+
+    if zero._comm is not None and zero._comm.timeout_ms > 0:
+        marked, packets = step_end_ms(False), step_end_ms(True)
+        out["step_end_window"] = {
+            "ms": marked, "ms_with_packets_r5": packets, "saved_us": (packets - marked) * 1e3,
+            "timing": "HIP events around zero.step() on the step's stream (median of 6 untimed steps): the update, "
+                      "the clip / overflow all-reduces and the parameter all-gathers; 'with_packets_r5': an event "
+                      "packet after every collective for the RCCL watchdog, as round 5"}
+    zero.wait_allgather()
     out["parity"] = PC.zero_parity_step(zero, fwd_bwd)
     zero.close()
     del zero, model

@@ -80,6 +80,8 @@ SIGNATURES = {
     "gs_reduce_scatter": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _vp]),
     "gs_all_gather": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp]),
     "gs_broadcast": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _vp]),
+    "gs_allreduce_marked": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _vp, _vp]),
+    "gs_all_gather_marked": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
     "gs_plan_create": (_c_int, [_c_int, _c_int, _c_int, _p_i64, _c_i64, _p_vp]),
     "gs_plan_create_ex": (_c_int, [_c_int, _c_int, _c_int, _p_i64, _c_i64, _c_i64, _p_vp]),
     "gs_plan_destroy": (_c_int, [_vp]),
@@ -150,6 +152,8 @@ SIGNATURES = {
     "gs_bucketer_last_timing": (_c_int, [_vp, _c_int, _p_f]),
     "gs_bucketer_set_timeline": (_c_int, [_vp, _c_int]),
     "gs_bucketer_bucket_stream": (_c_int, [_vp, _c_int, ctypes.POINTER(_vp)]),
+    "gs_bucketer_set_mark_consumer": (_c_int, [_vp, _vp]),
+    "gs_bucketer_first_pack_plan": (_c_int, [_vp, _p_vp]),
 }
 
 

@@ -131,8 +131,16 @@ class Communicator:
     def _s(self, stream):
         return self.stream_ptr if stream is None else stream
 
-    def all_reduce(self, t: torch.Tensor, op="sum", stream=None, out: torch.Tensor | None = None):
+    def all_reduce(self, t: torch.Tensor, op="sum", stream=None, out: torch.Tensor | None = None, consumer=None):
+        """consumer: a plan handle (c_void_p) whose next launch, stream-ordered after
+        this collective, carries its watchdog mark instead of an event packet
+        (gs_allreduce_marked)."""
         out = t if out is None else out
+        if consumer is not None:
+            L.check(L.lib().gs_allreduce_marked(self.handle, t.data_ptr(), out.data_ptr(), t.numel(),
+                                                L.gs_dtype(t.dtype), _REDUCE_OPS[op], self._s(stream), consumer),
+                    "gs_allreduce_marked")
+            return out
         L.check(L.lib().gs_allreduce(self.handle, t.data_ptr(), out.data_ptr(), t.numel(), L.gs_dtype(t.dtype),
                                      _REDUCE_OPS[op], self._s(stream)), "gs_allreduce")
         return out
@@ -143,7 +151,12 @@ class Communicator:
                 "gs_reduce_scatter")
         return recv
 
-    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream=None):
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream=None, consumer=None):
+        if consumer is not None:  # the mark rides on `consumer`'s next launch (gs_all_gather_marked)
+            L.check(L.lib().gs_all_gather_marked(self.handle, send.data_ptr(), recv.data_ptr(), send.numel(),
+                                                 L.gs_dtype(send.dtype), self._s(stream), consumer),
+                    "gs_all_gather_marked")
+            return recv
         L.check(L.lib().gs_all_gather(self.handle, send.data_ptr(), recv.data_ptr(), send.numel(),
                                       L.gs_dtype(send.dtype), self._s(stream)), "gs_all_gather")
         return recv

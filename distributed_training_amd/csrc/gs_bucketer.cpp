@@ -30,7 +30,7 @@ ncclComm_t comm_handle(gs_comm* c);
 hipStream_t comm_stream(gs_comm* c);
 int comm_dtype(int dt, ncclDataType_t* out);
 int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what,
-                 bool track = true);
+                 bool track = true, gs_plan* consumer = nullptr);
 int comm_track_event(gs_comm* c, hipEvent_t ev);
 bool comm_watching(gs_comm* c);
 void comm_forget_event(gs_comm* c, hipEvent_t ev);
@@ -132,6 +132,9 @@ struct gs_bucketer {
                                     // event of the producer-side tail's last kernel (done_on_chain)
   bool done_on_chain = false;
   bool tail_ran_on_producer = false;
+  // sharded buckets (no unpack): the plan whose next launch consumes the shards (ZeRO's
+  // update) carries the collectives' watchdog marks (gs_bucketer_set_mark_consumer)
+  gs_plan* mark_consumer = nullptr;
   std::mutex mu;
 
   bool hip() const { return kind == GS_DEV_HIP; }
@@ -230,7 +233,8 @@ int pack_one(gs_bucketer* b, Bucket& bk, void* stream) {
 
 // track = false: the caller hands the collective to the watchdog through an event
 // of its own that the stream records after it (comm_track_event)
-int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs, bool track = true) {
+// consumer (nullable): the plan whose next launch carries the collective's mark instead
+int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs, bool track = true, gs_plan* consumer = nullptr) {
   ncclDataType_t dt;
   GS_TRY_RET(comm_dtype(bk.bdt, &dt));
   if (b->flags & GS_BKT_REDUCE_SCATTER) {
@@ -238,11 +242,11 @@ int launch_collective(gs_bucketer* b, Bucket& bk, hipStream_t cs, bool track = t
     return comm_enqueue(b->comm, cs, [&] {
       return ncclReduceScatter(bk.buf, bk.shard, static_cast<size_t>(bk.numel / w), dt, ncclSum,
                                comm_handle(b->comm), cs);
-    }, "bucket reduce-scatter", track);
+    }, "bucket reduce-scatter", track, consumer);
   }
   return comm_enqueue(b->comm, cs, [&] {
     return ncclAllReduce(bk.buf, bk.buf, static_cast<size_t>(bk.numel), dt, ncclSum, comm_handle(b->comm), cs);
-  }, "bucket all-reduce", track);
+  }, "bucket all-reduce", track, consumer);
 }
 
 int launch_bucket(gs_bucketer* b, int bi) {
@@ -332,7 +336,8 @@ int launch_bucket(gs_bucketer* b, int bi) {
         if (chain_end) end_ev = b->done_ev = wd_ev;
       }
     }
-    GS_TRY_RET(launch_collective(b, bk, cs, wd_ev == nullptr));
+    // no unpack (sharded buckets): the shards' consumer, when named, carries the mark
+    GS_TRY_RET(launch_collective(b, bk, cs, wd_ev == nullptr, unpacks ? nullptr : b->mark_consumer));
     GS_TRY_RET(debug_sum(b, bk, 1, cs));
     // unpack: t1 a packet before it, its stop = u1 or the done mark; the collective lies
     // between t0 and t1
@@ -688,6 +693,21 @@ int gs_bucketer_set_timeline(gs_bucketer* b, int level) {
   std::lock_guard<std::mutex> lk(b->mu);
   if (b->prepared) return fail(GS_ESTATE, "gs_bucketer_set_timeline inside a backward");
   b->timeline = level;
+  return GS_OK;
+}
+
+int gs_bucketer_set_mark_consumer(gs_bucketer* b, gs_plan* consumer) {
+  GS_CHECK_ARG(b != nullptr, "gs_bucketer_set_mark_consumer: NULL bucketer");
+  std::lock_guard<std::mutex> lk(b->mu);
+  GS_CHECK_ARG(consumer == nullptr || !b->do_unpack(),
+               "gs_bucketer_set_mark_consumer: only sharded (NO_UNPACK / REDUCE_SCATTER) buckets hand marks on");
+  b->mark_consumer = consumer;
+  return GS_OK;
+}
+
+int gs_bucketer_first_pack_plan(gs_bucketer* b, gs_plan** out) {
+  GS_CHECK_ARG(b != nullptr && out != nullptr, "gs_bucketer_first_pack_plan: NULL argument");
+  *out = b->buckets.empty() ? nullptr : b->buckets[0].plan;
   return GS_OK;
 }
 

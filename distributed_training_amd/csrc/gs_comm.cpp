@@ -54,11 +54,22 @@ struct gs_comm {
   // entry per event, each standing for one record; a few of them are queried per poll
   std::vector<Inflight> caller;
   size_t caller_next = 0;  // rotation cursor over `caller`
+  // marks carried by consumer plans' launches (comm_mark_take): a ring, each slot
+  // re-recorded only after its previous record completed
+  std::vector<hipEvent_t> mark_ring;
+  size_t mark_next = 0;
   std::vector<hipEvent_t> ev_pool;
 };
 
 namespace gs {
 namespace {
+
+// live communicators: a consumer plan holds its deferring communicator's address
+// until its next launch, which checks here first (comm_mark_take), so a
+// communicator destroyed in between is never touched
+std::mutex g_live_mu;
+std::vector<gs_comm*> g_live;
+bool comm_live_locked(gs_comm* c) { return std::find(g_live.begin(), g_live.end(), c) != g_live.end(); }
 
 int rccl_fail(ncclResult_t r, const char* what) {
   return fail(GS_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
@@ -289,8 +300,11 @@ void comm_forget_event(gs_comm* c, hipEvent_t ev) {
 
 // Enqueue one RCCL collective under c->mu: liveness check, enqueue and
 // watchdog tracking are atomic with respect to the watchdog's abort.
+// consumer (nullable): the plan whose next launch is stream-ordered after this
+// collective; with a watchdog running (and not under capture) the collective's
+// mark is deferred to that launch's stop event instead of a packet after it.
 int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_t()>& fn, const char* what,
-                 bool track = true) {
+                 bool track = true, gs_plan* consumer = nullptr) {
   if (!c) return fail(GS_EINVAL, "no communicator");
   GsRange range(what);
   std::lock_guard<std::mutex> lk(c->mu);
@@ -299,7 +313,52 @@ int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_
   const ncclResult_t r = fn();
   c->enq_since.store(0);
   if (r != ncclSuccess) return rccl_fail(r, what);
-  return track ? comm_track_locked(c, stream) : GS_OK;
+  if (!track) return GS_OK;
+  if (consumer && consumer->kind == GS_DEV_HIP && consumer->n > 0 && !consumer->segs.empty() &&
+      c->timeout_ms > 0 && !stream_capturing(stream)) {
+    consumer->watch_comm = c;
+    return GS_OK;
+  }
+  return comm_track_locked(c, stream);
+}
+
+int comm_mark_take(gs_comm* c, void** ev) {
+  *ev = nullptr;
+  std::lock_guard<std::mutex> live(g_live_mu);
+  if (!c || !comm_live_locked(c)) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->timeout_ms <= 0 || c->aborted.load()) return 0;
+  constexpr size_t kRing = 16;
+  if (c->mark_ring.empty()) {
+    for (size_t i = 0; i < kRing; ++i) {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) break;
+      c->mark_ring.push_back(e);
+    }
+    if (c->mark_ring.empty()) return 1;  // no event: a pooled packet after the launch
+  }
+  hipEvent_t e = c->mark_ring[c->mark_next];
+  if (hipEventQuery(e) != hipSuccess) return 1;  // its previous record is still pending
+  c->mark_next = (c->mark_next + 1) % c->mark_ring.size();
+  *ev = e;
+  return 1;
+}
+
+int comm_mark_commit(gs_comm* c, void* ev, void* stream) {
+  std::lock_guard<std::mutex> live(g_live_mu);
+  if (!c || !comm_live_locked(c)) return GS_OK;
+  hipEvent_t e = static_cast<hipEvent_t>(ev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->timeout_ms <= 0) return GS_OK;
+  if (!e) return comm_track_locked(c, static_cast<hipStream_t>(stream));
+  const auto now = std::chrono::steady_clock::now();
+  for (auto& f : c->caller)
+    if (f.ev == e) {
+      f.t0 = now;
+      return GS_OK;
+    }
+  c->caller.push_back({e, now});
+  return GS_OK;
 }
 
 }  // namespace gs
@@ -354,12 +413,20 @@ int gs_comm_create_ex(int rank, int world, const uint8_t* uid, int device, int m
     delete c;
     return rccl_fail(r, "ncclCommInitRank");
   }
+  {
+    std::lock_guard<std::mutex> live(g_live_mu);
+    g_live.push_back(c);
+  }
   *out = c;
   return GS_OK;
 }
 
 int gs_comm_destroy(gs_comm* c) {
   if (!c) return GS_OK;
+  {
+    std::lock_guard<std::mutex> live(g_live_mu);
+    g_live.erase(std::remove(g_live.begin(), g_live.end(), c), g_live.end());
+  }
   if (c->wd.joinable()) {
     c->wd_stop.store(true);
     c->wd.join();
@@ -368,6 +435,7 @@ int gs_comm_destroy(gs_comm* c) {
   if (c->stream && !c->aborted.load()) (void)hipStreamSynchronize(c->stream);
   for (auto& f : c->pooled) (void)hipEventDestroy(f.ev);  // the caller's events stay the caller's
   for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : c->mark_ring) (void)hipEventDestroy(ev);
   if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -437,6 +505,28 @@ int gs_allreduce(gs_comm* c, const void* send, void* recv, int64_t count, int dt
   hipStream_t s = pick(c, stream);
   return comm_enqueue(c, s, [&] { return ncclAllReduce(send, recv, static_cast<size_t>(count), dt, o, c->comm, s); },
                       "ncclAllReduce");
+}
+
+int gs_allreduce_marked(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op, void* stream,
+                        gs_plan* consumer) {
+  GS_CHECK_ARG(c != nullptr, "gs_allreduce_marked: NULL communicator");
+  ncclDataType_t dt;
+  ncclRedOp_t o;
+  GS_TRY_RET(to_nccl_dtype(dtype, &dt));
+  GS_TRY_RET(to_nccl_op(op, &o));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(c, s, [&] { return ncclAllReduce(send, recv, static_cast<size_t>(count), dt, o, c->comm, s); },
+                      "ncclAllReduce", true, consumer);
+}
+
+int gs_all_gather_marked(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype, void* stream,
+                         gs_plan* consumer) {
+  GS_CHECK_ARG(c != nullptr, "gs_all_gather_marked: NULL communicator");
+  ncclDataType_t dt;
+  GS_TRY_RET(to_nccl_dtype(dtype, &dt));
+  hipStream_t s = pick(c, stream);
+  return comm_enqueue(c, s, [&] { return ncclAllGather(send, recv, static_cast<size_t>(send_count), dt, c->comm, s); },
+                      "ncclAllGather", true, consumer);
 }
 
 int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_count, int dtype,

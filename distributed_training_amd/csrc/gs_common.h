@@ -203,6 +203,9 @@ struct gs_plan {
   // that kernel's own dispatch (hipExtLaunchKernel start / stop), not as packets
   void* once_start = nullptr;
   void* once_stop = nullptr;
+  // a collective's watchdog mark rides on this plan's next eager launch (its stop event):
+  // the communicator that deferred it there (gs_allreduce_marked & co.), or NULL
+  void* watch_comm = nullptr;
   unsigned long long table_capture_id = 0;  // capture that last recorded a table write
   bool in_graph = false;        // a graph holds a table write: re-upload before eager launches
   const float* hyper = nullptr; // device hyper-parameter source of sgd/adam (gs_plan_set_hyper_source)
@@ -268,6 +271,15 @@ GS_HD inline void adam_hyper_update(double* step, const double* lr, double beta1
 }
 int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, double wd,
                    const float* found_inf, float* hyper, void* stream);
+
+// Deferred watchdog marks (gs_comm.cpp): a consumer plan's launch carries the mark of
+// the collectives deferred to it.  comm_mark_take: 0 = nothing to do (the
+// communicator is gone or not watching), 1 = carry *ev as the launch's stop event
+// (*ev NULL: every mark of the ring is still pending — comm_mark_commit then records a
+// pooled packet after the launch instead).  comm_mark_commit hands the carried event
+// (or that packet) to the watchdog.
+int comm_mark_take(gs_comm* c, void** ev);
+int comm_mark_commit(gs_comm* c, void* ev, void* stream);
 
 // HIP-side implementations (gs_kernels.hip)
 int hip_plan_upload_static(gs_plan* p);

@@ -1198,12 +1198,24 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   const bool once = !capturing && (p->once_start != nullptr || p->once_stop != nullptr);
   const int nslots = (capturing || once) ? 0 : static_cast<int>(p->timer_ev.size() / 2);
   const int tk = p->timer_next;
-  const bool ext = once || nslots;
   hipEvent_t ev0 = once ? static_cast<hipEvent_t>(p->once_start)
                         : nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk]) : nullptr;
   hipEvent_t ev1 = once ? static_cast<hipEvent_t>(p->once_stop)
                         : nslots ? static_cast<hipEvent_t>(p->timer_ev[2 * tk + 1]) : nullptr;
   p->once_start = p->once_stop = nullptr;
+  // a collective deferred its watchdog mark to this launch (gs_allreduce_marked,
+  // gs_bucketer_set_mark_consumer): the kernel's own stop event carries it when the
+  // launch has none of its own, else a packet follows the launch
+  gs_comm* wc = (!capturing && p->watch_comm) ? static_cast<gs_comm*>(p->watch_comm) : nullptr;
+  void* wev = nullptr;
+  int wtake = 0;
+  if (wc) {
+    p->watch_comm = nullptr;
+    wtake = comm_mark_take(wc, &wev);
+  }
+  const bool wcarry = wtake && wev && ev1 == nullptr;
+  if (wcarry) ev1 = static_cast<hipEvent_t>(wev);
+  const bool ext = once || nslots || wcarry;
   bool fused = false;
   int grid = 1;
   {
@@ -1256,6 +1268,10 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
                            (const float*)p->d_partials, grid, red_out, accumulate);
       HIP_RET(hipGetLastError());
     }
+  }
+  if (wtake) {
+    if (wev && !wcarry) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(wev), s));
+    GS_TRY_RET(comm_mark_commit(wc, wev, stream));
   }
   if (nslots) {
     p->timer_kind[tk] = Op::kKind;

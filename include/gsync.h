@@ -139,6 +139,20 @@ int gs_reduce_scatter(gs_comm* c, const void* send, void* recv, int64_t recv_cou
                       int op, void* stream);
 int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
                   void* stream);
+/* The same collectives with their watchdog mark deferred to a consumer kernel:
+ * with a watchdog running, no event packet follows the collective (~4.7 µs of
+ * stream time on the step's end each); `consumer`'s next launch
+ * carries the communicator's mark as its own stop event instead and hands it
+ * to the watchdog.  The caller guarantees that launch is stream-ordered after
+ * the collective (ZeRO: the partials all-reduce before the clipped update on the
+ * same stream; the parameter all-gather before the next backward's first pack).
+ * NULL consumer (or an empty plan, a capture): a packet, as the entry points above.
+ * replaces: ProcessGroupNCCL's per-work end event (T:.../ProcessGroupNCCL.hpp:424
+ *           ncclEndEvent_), recorded after every collective */
+int gs_allreduce_marked(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
+                        void* stream, gs_plan* consumer);
+int gs_all_gather_marked(gs_comm* c, const void* send, void* recv, int64_t send_count, int dtype,
+                         void* stream, gs_plan* consumer);
 int gs_broadcast(gs_comm* c, const void* send, void* recv, int64_t count, int dtype, int root,
                  void* stream);
 
@@ -402,6 +416,17 @@ int gs_bucketer_set_found_inf(gs_bucketer* b, float* found_inf);
  * _set_forward_pass_work_handle). */
 int gs_bucketer_set_div_factor(gs_bucketer* b, float div_factor);
 int gs_bucketer_unpack_bucket(gs_bucketer* b, int bucket, void* stream);
+/* Sharded buckets (NO_UNPACK / REDUCE_SCATTER, the ZeRO engine): the
+ * bucket collectives' watchdog marks ride on `consumer`'s next launch (the
+ * sharded update, stream-ordered after finalize) instead of a packet after
+ * each collective; NULL restores the packets.  GS_EINVAL on unpacking buckets
+ * (their unpack kernels already carry the marks).
+ * replaces: ProcessGroupNCCL's per-work end event, as gs_allreduce_marked */
+int gs_bucketer_set_mark_consumer(gs_bucketer* b, gs_plan* consumer);
+/* the plan of bucket 0's pack — the first libgsync kernel of the next
+ * synchronising backward, a consumer for collectives issued after a step
+ * (ZeRO's parameter all-gather) */
+int gs_bucketer_first_pack_plan(gs_bucketer* b, gs_plan** out);
 /* timing of the library's own collective launches (ms of the last iteration, via events) */
 int gs_bucketer_last_comm_ms(gs_bucketer* b, int bucket, float* ms);
 /* per-bucket timeline of the last iteration (HIP events; -1 where untimed:

@@ -45,3 +45,20 @@ def test_every_script_is_cited():
         if os.path.isdir(path) or f.startswith("."):
             continue
         assert re.search(r"(?<![A-Za-z0-9_])" + re.escape(f), text), f"scripts/{f} is cited nowhere"
+
+
+def test_leg_cost_scales_with_world_size():
+    """The wall-budget skip rule's leg estimates grow with the ranks:
+    at one GPU per rank by the per-rank growth and communicator set-up, under the gloo
+    rehearsal by the ranks sharing each GPU as well."""
+    code = ("import sys; sys.argv=['bench.py']; sys.path.insert(0, %r); import bench\n"
+            "for leg in bench.LEG_COST_S:\n"
+            "    c1 = bench.leg_cost(leg, 1, 'nccl')\n"
+            "    c8 = bench.leg_cost(leg, 8, 'nccl')\n"
+            "    g8 = bench.leg_cost(leg, 8, 'gloo', ranks_per_gpu=8)\n"
+            "    assert c1 == max(5.0, bench.LEG_COST_S[leg]), leg\n"
+            "    assert c8 >= c1 * (1 + 7 * bench.LEG_GROWTH_PER_RANK) - 1e-9 or c8 == 5.0, leg\n"
+            "    assert g8 >= 8 * c8 - 8 * 7 * bench.LEG_FIXED_PER_RANK_S.get(leg, 0.0) - 1e-9 or g8 == 5.0, leg\n"
+            "print('ok')" % REPO)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]
