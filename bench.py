@@ -295,6 +295,29 @@ def _kernel_rows(shapes, dev, iters):
     up.set_clip(None)
     rows["clip_path_sgd"] = {"alg_bytes": 24 * n, "avg_ms": ms, "GBps": 24 * n / (ms * 1e-3) / 1e9,
                              "launches": "sqnorm_partial + clipped sgd"}
+    # clip_grad_norm_ as the drop-in runs it (T:nn/utils/clip_grad.py:165-174; the clip the
+    # DeepSpeed config sets, R:resnet/deepspeed/deepspeed_train.py:195): the Σg² partial sums,
+    # then the scale pass whose workgroups fold them (two launches, both timed); clipping
+    # active (max_norm below ‖g‖: read 4 + read/write 8 B per element), the grads restored
+    # by an untimed copy before each call
+    from distributed_training_amd import optim as OPT
+
+    cps = [torch.nn.Parameter(torch.empty(s, device=dev)) for s in shapes]
+    cgs = [gr.clone() for gr in grads]
+    for p_, g_ in zip(cps, cgs):
+        p_.grad = g_
+    OPT.clip_grad_norm_(cps, 1e-3)
+    cplan = OPT._NORM_PLANS[tuple(numels) + (cgs[0].device,)]
+
+    def clip_call():
+        torch._foreach_copy_(cgs, grads)
+        OPT.clip_grad_norm_(cps, 1e-3)
+
+    ms = rate(clip_call, cplan)
+    rows["clip_grad_norm"] = {"alg_bytes": 12 * n, "avg_ms": ms, "GBps": 12 * n / (ms * 1e-3) / 1e9,
+                              "launches": "sqnorm_partial + clip_scale (the coefficient folded per workgroup)",
+                              "restore": "an untimed copy of the grads before each call"}
+    del cps, cgs
     up.set_ptrs(3, vs)
     ms = rate(lambda: up.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5), up)
     rows["adam"] = {"alg_bytes": 28 * n, "avg_ms": ms, "GBps": 28 * n / (ms * 1e-3) / 1e9}

@@ -106,6 +106,7 @@ SIGNATURES = {
     "gs_plan_set_read_hint": (_c_int, [_vp, _c_int]),
     "gs_sqnorm_partial_out": (_c_int, [_vp, _c_int, _c_int, _vp, _p_i32, _vp]),
     "gs_plan_set_clip_groups": (_c_int, [_vp, _vp, ctypes.c_int32, _c_f, _c_f, _c_f, _c_f, _vp]),
+    "gs_clip_scale": (_c_int, [_vp, _c_int, _c_int, _vp]),
     "gs_rng_state_bytes": (_c_int, []),
     "gs_rng_draw_u32": (_c_int, [_vp, _c_i64, _c_i64, _vp]),
     "gs_randperm": (_c_int, [ctypes.c_uint64, _c_i64, _vp]),

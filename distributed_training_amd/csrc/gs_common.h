@@ -152,6 +152,9 @@ struct ClipArgs {
   float max_norm, eps;
   float sq_mul, coef_mul;  // host multipliers (ZeRO's loss scale): 1 = none
   float* out;          // [sq, coef, norm] written by workgroup 0 (nullable)
+  // 0: DeepSpeed's `if coef < 1: clip` (a NaN coefficient clips nothing); 1: torch's
+  // clamp(coef, max=1) (clip_grad_norm_, T:nn/utils/clip_grad.py:172 — NaN stays NaN)
+  int32_t torch_clamp;
 };
 
 inline SgdHyper make_sgd(double lr, double mom, double damp, double wd, int nest, int maxi,
@@ -301,6 +304,7 @@ int hip_clip_coef(const float* sq, float max_norm, float eps, float* coef, float
                   void* stream);
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
                       void* stream);
+int hip_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream);
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream);
 const float* hip_plan_red_groups(const gs_plan* p);  // the 64 group sums of gs_sqnorm_partial
 float* hip_plan_red_scalar(const gs_plan* p);        // its finished Σ when red_groups == 0
@@ -318,6 +322,7 @@ int host_unpack(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst
                 int acc);
 int host_unpack_check(gs_plan* p, const void* flat, int flat_dt, int dst_slot, int dst_dt, float* found);
 int host_scale(gs_plan* p, int slot, int dt, float s, int mode);
+int host_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip);
 int host_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc);
 int host_sum(gs_plan* p, int slot, int dt, float* out, int acc);
 int host_clip_coef(const float* sq, float max_norm, float eps, float* coef, float* norm);

@@ -951,6 +951,39 @@ struct UnscaleOp {
   }
 };
 
+// clip_grad_norm_'s scale pass (gs_clip_scale): x *= the clip coefficient, which every
+// workgroup forms itself from the plan's Σg² partial sums (clip_multiplier, as the
+// clipped updates fold them: no combine and no coefficient launch between the Σg²
+// pass and this one).  A coefficient of exactly 1 leaves every element as it is
+// (x * 1 == x, NaN and -0 included), so the grid then exits before any access.
+template <int N, int DT>
+struct ClipScaleOp {
+  static constexpr int kN = N;
+  static constexpr int kG = GS_G_UNPACK;
+  static constexpr int kRed = 0;
+  static constexpr int kRedGrid = kGridLimit;
+  static constexpr int kRedFuseGrid = GS_RED_FUSE_GRID;
+  static constexpr int kKind = GS_OP_SCALE;
+  float* partials = nullptr;
+  int slot;
+  ClipArgs clip{};
+  float gsv = 1.f;
+  struct Frag { float x[N]; };
+  __device__ int phys(int k) const { return k == 0 ? slot : k; }
+  __device__ bool active() const { return gsv != 1.f; }  // uniform; a NaN coefficient scales
+  __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
+  template <bool F>
+  __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
+    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+  template <bool F>
+  __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) f.x[i] = f.x[i] * gsv;
+    st<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+  }
+};
+
 // SGD: slots 0 = p (f32), 1 = g (GD), 2 = momentum buffer (f32), 3 = low-precision copy (LD)
 // NTG: non-temporal loads of the grad (the load policy above; p and the state stay cached)
 template <int N, int GD, int LD, bool NTG = true>
@@ -1099,7 +1132,7 @@ __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float*
     sq = sq * c.sq_mul;
     const float nrm = sqrtf(sq);
     float coef = c.max_norm / (nrm + c.eps);
-    coef = coef < 1.f ? coef : 1.f;
+    coef = c.torch_clamp ? (coef >= 1.f ? 1.f : coef) : (coef < 1.f ? coef : 1.f);
     if (gscale) coef = coef * s;
     coef = coef * c.coef_mul;
     if (threadIdx.x == 0) {
@@ -1118,6 +1151,10 @@ template <class Op>
 __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
+}
+template <int N, int DT>
+__device__ __forceinline__ void load_hyper(ClipScaleOp<N, DT>& op) {
+  op.gsv = clip_multiplier(op.clip, nullptr);
 }
 template <int N, int GD, int LD, bool NTG>
 __device__ __forceinline__ void load_hyper(SgdOp<N, GD, LD, NTG>& op) {

@@ -201,6 +201,12 @@ int host_scale(gs_plan* p, int s_, int dt, float s, int mode) {
   return GS_OK;
 }
 
+int host_clip_scale(gs_plan* p, int s_, int dt, const ClipArgs& clip) {
+  const float cf = host_clip_factor(clip, nullptr);
+  if (cf == 1.f) return GS_OK;  // x * 1 == x: nothing to write (the device grid exits too)
+  return host_scale(p, s_, dt, cf, GS_SCALE_MUL);
+}
+
 int host_sqnorm(gs_plan* p, int s_, int dt, float* sq, int acc) {
   GS_HOST_FLOAT(dt, DT, {
     double total = 0.0;
@@ -289,7 +295,7 @@ float host_clip_factor(const ClipArgs& c, const float* gsc) {
   sq = sq * c.sq_mul;
   const float nrm = std::sqrt(sq);
   float coef = c.max_norm / (nrm + c.eps);
-  coef = coef < 1.f ? coef : 1.f;
+  coef = c.torch_clamp ? (coef >= 1.f ? 1.f : coef) : (coef < 1.f ? coef : 1.f);
   if (gsc) coef = coef * s;
   coef = coef * c.coef_mul;
   if (c.out) {

@@ -415,6 +415,17 @@ int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, d
   return GS_OK;
 }
 
+int hip_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream) {
+  DeviceGuard g(p->device);
+  GS_DISPATCH_FLOAT(dt, DT, {
+    ClipScaleOp<kUnit, DT> op;
+    op.slot = slot;
+    op.clip = clip;
+    return launch(p, op, stream);
+  });
+  return GS_OK;
+}
+
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
                       void* stream) {
   DeviceGuard g(p->device);

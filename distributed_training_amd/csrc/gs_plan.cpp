@@ -437,6 +437,20 @@ static int plan_clip(gs_plan* p, ClipArgs* c, const ClipArgs** out) {
   return GS_OK;
 }
 
+int gs_clip_scale(gs_plan* p, int slot, int dtype, void* stream) {
+  GsRange r("gs_clip_scale");
+  PLAN_OK(p);
+  SLOT_OK(slot);
+  GS_CHECK_ARG(p->clip_on, "gs_clip_scale: no clip set on the plan (gs_plan_set_clip / gs_plan_set_clip_groups)");
+  ClipArgs cs;
+  const ClipArgs* clip;
+  GS_TRY_RET(plan_clip(p, &cs, &clip));
+  cs = *clip;
+  cs.torch_clamp = 1;  // torch.clamp(coef, max=1): a NaN norm scales every grad by NaN, as torch
+  if (p->kind == GS_DEV_HOST) return host_clip_scale(p, slot, dtype, cs);
+  return hip_clip_scale(p, slot, dtype, cs, stream);
+}
+
 int gs_sum(gs_plan* p, int slot, int dtype, float* sum_dev, int accumulate, void* stream) {
   PLAN_OK(p);
   SLOT_OK(slot);

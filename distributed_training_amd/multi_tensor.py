@@ -228,6 +228,12 @@ class TensorListPlan:
             "gs_sum",
         )
 
+    def clip_scale(self, slot, dtype, stream=None):
+        """slot *= torch.clamp(max_norm/(‖g‖+eps), max=1) from this plan's clip
+        (:meth:`set_clip`, consumed like a clipped update's); nothing written when
+        the coefficient is 1 (gs_clip_scale)."""
+        L.check(L.lib().gs_clip_scale(self.handle, slot, L.gs_dtype(dtype), self._stream(stream)), "gs_clip_scale")
+
     def unscale_check(self, slot, dtype, inv_scale: torch.Tensor | None, found_inf: torch.Tensor, stream=None):
         L.check(
             L.lib().gs_unscale_check(self.handle, slot, L.gs_dtype(dtype),

@@ -561,9 +561,16 @@ def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm:
                     error_if_nonfinite: bool = False, foreach=None) -> torch.Tensor:
     """torch.nn.utils.clip_grad_norm_ for the L2 norm on libgsync kernels.
 
-    total_norm = ‖concat(g)‖₂ ; coef = min(1, max_norm / (total_norm + 1e-6));
+    total_norm = ‖concat(g)‖₂ ; coef = clamp(max_norm / (total_norm + 1e-6), max=1);
     grads *= coef (T:nn/utils/clip_grad.py:165-174).  Everything stays on the
     device; only error_if_nonfinite forces a host read, as in torch.
+
+    One grad dtype (the common case) is two launches: the Σg² partial sums
+    (gs_sqnorm_partial, left in the plan), then the scale pass whose every
+    workgroup folds them into the coefficient itself (gs_clip_scale; it writes
+    nothing when the coefficient is 1).  No combine launch, no coefficient
+    launch, no flag fill.  Several grad dtypes: Σg² accumulated over the groups
+    (gs_sqnorm), then each group's scale pass folds that scalar.
     """
     if isinstance(parameters, torch.Tensor):
         parameters = [parameters]
@@ -578,10 +585,11 @@ def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm:
         if not is_dense(g):
             raise RuntimeError("clip_grad_norm_: grads must be dense")
         groups.setdefault(g.dtype, []).append(g)
-    buf = torch.zeros(3, dtype=torch.float32, device=dev)
-    sq, coef, norm = buf[0:1], buf[1:2], buf[2:3]
+    # [Σg², coef, norm | accumulated Σg² (several dtypes)]: written by the kernels before
+    # any read (workgroup 0 of the scale pass publishes the first three), so no fill
+    buf = torch.empty(4, dtype=torch.float32, device=dev)
     plans = []
-    for i, (dt, gl) in enumerate(groups.items()):
+    for dt, gl in groups.items():
         key = tuple(g.numel() for g in gl) + (dev,)  # sizes + device: grad ids are reused after zero_grad
         plan = _NORM_PLANS.get(key)
         if plan is None:
@@ -590,19 +598,27 @@ def clip_grad_norm_(parameters: torch.Tensor | Iterable[torch.Tensor], max_norm:
                 _NORM_PLANS.clear()
             _NORM_PLANS[key] = plan
         plan.set_ptrs(0, gl)
-        plan.sqnorm(0, dt, sq, accumulate=i > 0)
         plans.append((plan, dt))
-    clip_coef(sq, float(max_norm), 1e-6, coef, norm)
-    if error_if_nonfinite and not torch.isfinite(norm).item():
-        raise RuntimeError(
-            f"The total norm of order {float(norm_type)} for gradients from `parameters` is non-finite, "
-            "so it cannot be clipped. To disable this error and scale the gradients by the non-finite "
-            "norm anyway, set `error_if_nonfinite=False`")
+    if len(plans) == 1 and not error_if_nonfinite:
+        plan, dt = plans[0]
+        plan.sqnorm_partial(0, dt)
+        plan.set_clip(float(max_norm), 1e-6, None, out=buf[0:3])
+    else:
+        raw = buf[3:4]
+        for i, (plan, dt) in enumerate(plans):
+            plan.sqnorm(0, dt, raw, accumulate=i > 0)
+        # torch raises before touching the grads (T:nn/utils/clip_grad.py:96-109)
+        if error_if_nonfinite and not torch.isfinite(raw).item():
+            raise RuntimeError(
+                f"The total norm of order {float(norm_type)} for gradients from `parameters` is non-finite, "
+                "so it cannot be clipped. To disable this error and scale the gradients by the non-finite "
+                "norm anyway, set `error_if_nonfinite=False`")
+        for plan, _ in plans:
+            plan.set_clip(float(max_norm), 1e-6, raw, out=buf[0:3])
     for plan, dt in plans:
-        # grads *= coef: a unit-scale SGD step is not the right tool; use the
-        # unscale kernel with the coefficient as the (device) multiplier
-        found = torch.zeros(1, dtype=torch.float32, device=dev)
-        plan.unscale_check(0, dt, coef, found)
+        plan.clip_scale(0, dt)
+        plan.set_clip(None)
+    norm = buf[2:3]
     # the kernel wrote the grads in place: tell autograd's version counters, as a
     # torch in-place op would (a DDP's fused Σg² of these grads is stale now)
     increment_version(grads)

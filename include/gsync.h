@@ -292,6 +292,15 @@ int gs_sqnorm_partial_out(gs_plan* p, int slot, int dtype, float* groups_out, in
  * reduction's own 64-lane tree — so every rank forms the same coefficient. */
 int gs_plan_set_clip_groups(gs_plan* p, const float* groups_dev, int32_t n_groups, float max_norm,
                             float eps, float sq_mul, float coef_mul, float* out_dev);
+/* clip_grad_norm_'s scale pass: slot `slot` (dtype) *= the clip coefficient of
+ * the plan's clip (gs_plan_set_clip / gs_plan_set_clip_groups, consumed as by a
+ * clipped update), torch.clamp(max_norm / (‖g‖ + eps), max = 1): every
+ * workgroup folds the Σg² partial sums itself, workgroup 0 publishes
+ * [Σg², coef, norm] to the clip's out; a coefficient of exactly 1 writes
+ * nothing (x * 1 == x).  With gs_sqnorm_partial before it, clip_grad_norm_ is
+ * two launches: no combine, no coefficient kernel, no flag fill.
+ * replaces: T:nn/utils/clip_grad.py:165-174 (clip_coef, clamp, _foreach_mul_) */
+int gs_clip_scale(gs_plan* p, int slot, int dtype, void* stream);
 /* coef_dev[0] = min(1, max_norm / (sqrt(sqnorm_dev[0]) + eps)); norm_dev (nullable) = sqrt
  * replaces: T:nn/utils/clip_grad.py:165-174 clip_coef / clamp */
 int gs_clip_coef(int device_kind, const float* sqnorm_dev, float max_norm, float eps,

@@ -218,6 +218,52 @@ def test_clip_grad_norm_matches_torch(cuda_device):
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("case", ["clip", "no_clip", "nan", "bf16"])
+def test_clip_grad_norm_two_launches(cuda_device, case):
+    """The drop-in clip_grad_norm_ is two launches on one grad dtype:
+    the Σg² partial sums, then the scale pass whose workgroups fold them into the
+    coefficient themselves — no combine, no coefficient launch, no flag fill.  The
+    published [Σg², coef, norm] follow torch's arithmetic (coef = clamp(max/(norm +
+    1e-6), max=1) in fp32), the grads are g * coef bit for bit; a coefficient of 1
+    leaves them untouched, a NaN norm makes them NaN (torch.clamp keeps NaN)."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd import optim as OPT
+
+    dt = torch.bfloat16 if case == "bf16" else torch.float32
+    sizes = [10, 3000, 7, 70_000, 1 << 20]
+    gs = rand_list(sizes, dt, cuda_device, seed=21, scale=5.0)
+    if case == "nan":
+        gs[1][5] = float("nan")
+    ps = [torch.nn.Parameter(torch.zeros(n, device=cuda_device, dtype=dt)) for n in sizes]
+    for p, g in zip(ps, gs):
+        p.grad = g.clone()
+    max_norm = 1e9 if case == "no_clip" else 1.0
+    OPT.clip_grad_norm_(ps, max_norm)  # builds the cached plan
+    plan = OPT._NORM_PLANS[tuple(sizes) + (cuda_device,)]
+    for p, g in zip(ps, gs):
+        p.grad.copy_(g)
+    torch.cuda.synchronize()
+    plan.timer_enable(8)
+    norm = OPT.clip_grad_norm_(ps, max_norm)
+    torch.cuda.synchronize()
+    kinds = plan.timer_read_by_kind()
+    plan.timer_enable(0)
+    assert sorted((k, len(v)) for k, v in kinds.items()) == [(L.GS_OP_SCALE, 1), (L.GS_OP_SQNORM, 1)], kinds
+    want_sq = O.sqnorm([to_np(g.float()) for g in gs])
+    if case == "nan":
+        assert torch.isnan(norm).item()
+        assert all(torch.isnan(p.grad.float()).all().item() for p in ps)
+        return
+    assert abs(norm.item() - want_sq ** 0.5) <= 1e-5 * want_sq ** 0.5
+    buf_norm = norm.reshape(1)
+    nrm = torch.tensor([norm.item()], dtype=torch.float32)
+    coef = torch.clamp(torch.tensor([max_norm], dtype=torch.float32) / (nrm + 1e-6), max=1.0)
+    for p, g in zip(ps, gs):
+        want = g if coef.item() == 1.0 else (g.float() * coef.item()).to(dt)
+        assert torch.equal(p.grad, want)
+    assert buf_norm.device == cuda_device
+
+
 def test_large_sgd_property(cuda_device):
     """ResNet-152-sized flat step (60.2M params, > Infinity Cache): bit-exact vs the oracle."""
     n = 60_192_808

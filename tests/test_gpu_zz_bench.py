@@ -157,7 +157,7 @@ def _check_line(d, n):
     assert set(k["kernels"]) == {"pack_f32", "pack_f32_to_bf16", "unpack_f32", "unpack_f32+sqnorm", "sqnorm_f32",
                                  "sqnorm_f32_after_unpack", "sqnorm_f32_after_unpack_nt",
                                  "pack_bf16", "unpack_bf16_to_f32", "sgd_momentum_wd", "sqnorm_partial_f32",
-                                 "clip_path_sgd", "adam"}
+                                 "clip_path_sgd", "adam", "clip_grad_norm"}
     # the folded clip path: Σg² partials + the clipped update, both launches in one row
     assert k["kernels"]["clip_path_sgd"]["alg_bytes"] == 24 * d["config"]["params"]
     assert k["kernels"]["clip_path_sgd"]["avg_ms"] > k["kernels"]["sgd_momentum_wd"]["avg_ms"]
