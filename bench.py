@@ -201,7 +201,7 @@ def collective_bench(ddp, zero, world, iters=10, warmup=3):
             "timing": "HIP events on libgsync's comm stream, median of 10 after 3 warmup, ops back to back"}
 
 
-def _kernel_rows(shapes, dev, iters):
+def _kernel_rows(shapes, dev, iters, shapes16=None):
     """Every grad-sync kernel of the step on one parameter set (shapes), warm and
     alone on the GPU: pack fp32 x1/ws, pack to bf16, unpack (+ fused Σg²), Σg² on
     a bucket-layout plan (64-element alignment, as the DDP buckets), the update
@@ -261,15 +261,27 @@ def _kernel_rows(shapes, dev, iters):
                       "read_hint": "the size rule (cached below 256 MiB)" if hint == 0 else "non-temporal"}
     plan.set_read_hint(0)
     # the 16-bit bucket paths: ZeRO's bf16 grads -> bf16 bucket (configs[3]) and the bf16
-    # bucket -> fp32 grads unpack (DDP bucket_dtype=bf16)
-    grads16 = [gr.to(torch.bfloat16) for gr in grads]
-    plan.set_ptrs(1, grads16)
-    ms = rate(lambda: plan.pack(1, torch.bfloat16, flat16, 0.125, 1), plan)
-    rows["pack_bf16"] = {"alg_bytes": 4 * n, "avg_ms": ms, "GBps": 4 * n / (ms * 1e-3) / 1e9}
-    plan.set_ptrs(1, grads)
-    ms = rate(lambda: plan.unpack(flat16, 1, torch.float32), plan)
-    rows["unpack_bf16_to_f32"] = {"alg_bytes": 6 * n, "avg_ms": ms, "GBps": 6 * n / (ms * 1e-3) / 1e9}
-    del flat, flat16, grads16
+    # bucket -> fp32 grads unpack (DDP bucket_dtype=bf16).  shapes16: their own (larger)
+    # parameter set, so that a 16-bit source is past the Infinity Cache too
+    if shapes16 is None:
+        plan16, n16, g32, f16 = plan, n, grads, flat16
+    else:
+        del flat, flat16
+        numels16 = [int(torch.Size(s_).numel()) for s_ in shapes16]
+        n16 = sum(numels16)
+        plan16 = TensorListPlan(numels16, dev, align=64)
+        g32 = [torch.randn(s_, device=dev, generator=g) * 0.01 for s_ in shapes16]
+        f16 = torch.zeros(plan16.flat_numel, device=dev, dtype=torch.bfloat16)
+    grads16 = [gr.to(torch.bfloat16) for gr in g32]
+    plan16.set_ptrs(1, grads16)
+    ms = rate(lambda: plan16.pack(1, torch.bfloat16, f16, 0.125, 1), plan16)
+    rows["pack_bf16"] = {"alg_bytes": 4 * n16, "avg_ms": ms, "GBps": 4 * n16 / (ms * 1e-3) / 1e9, "elems": n16}
+    plan16.set_ptrs(1, g32)
+    ms = rate(lambda: plan16.unpack(f16, 1, torch.float32), plan16)
+    rows["unpack_bf16_to_f32"] = {"alg_bytes": 6 * n16, "avg_ms": ms, "GBps": 6 * n16 / (ms * 1e-3) / 1e9,
+                                  "elems": n16}
+    del f16, grads16, g32, plan16
+    torch.cuda.empty_cache()
     up = TensorListPlan(numels, dev, task_units=update_task_units(dev))
     ps = [torch.randn(s, device=dev, generator=g) for s in shapes]
     bs = [torch.randn(s, device=dev, generator=g) * 0.01 for s in shapes]
@@ -516,13 +528,15 @@ def grad_sync_kernel_rates(params, dev, iters=20, comm=None, world=1):
     covers all of them, not just the headline update kernel.  With the engine's
     one-rank RCCL communicator: configs[3]'s N>1 clip path at its N=8 shard."""
     n, rows = _kernel_rows([tuple(p.shape) for p in params], dev, iters)
-    n_big, big = _kernel_rows(_beyond_ic_shapes(), dev, iters)
+    n_big, big = _kernel_rows(_beyond_ic_shapes(), dev, iters, shapes16=_beyond_ic_shapes() * 2)
     torch.cuda.empty_cache()
     out = {"params": n, "kernels": rows, "peak_GBps": HBM_PEAK_GBPS, "iters": iters,
            "timing": "after the timed region, warm, alone on the GPU; plan launch timer (the kernels' own start "
                      f"and end: hipExtLaunchKernel's HIP events on the launch stream), average of {iters} calls",
            "min_frac": min(r["frac"] for r in rows.values()),
-           "beyond_ic": {"params": n_big, "set": "ResNet-152 parameter shapes x 2 (> 256 MiB Infinity Cache)",
+           "beyond_ic": {"params": n_big, "set": "ResNet-152 parameter shapes x 2 (> 256 MiB Infinity Cache); the "
+                                               "16-bit-source rows (pack_bf16, unpack_bf16_to_f32) on x 4: a 481 MB "
+                                               "bf16 source",
                          "kernels": big, "min_frac": min(r["frac"] for r in big.values())}}
     if comm is not None and world == 1:
         out.update(zero_clip_path_rows(n, dev, comm, iters=iters))
