@@ -377,15 +377,17 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
     def adam():
         plan.adam(torch.bfloat16, 1e-3, 0.8, 0.999, 1e-8, 3e-7, True, False, -1e-3, 0.5, lowp_dtype=torch.bfloat16)
 
+    # as zero.py since round 6: the all-reduce's watchdog mark rides on the update kernel
+    # (gs_allreduce_marked), in both forms
     def folded():  # as zero.py: the whole partial-sum buffer travels and is folded
         plan.sqnorm_partial_out(1, torch.bfloat16, groups)
-        comm.all_reduce(groups, stream=stream)
+        comm.all_reduce(groups, stream=stream, consumer=plan.handle)
         plan.set_clip_groups(1.0, 1e-6, groups, groups.numel(), out=out)
         adam()
 
     def scalar():
         plan.sqnorm(1, torch.bfloat16, sq)
-        comm.all_reduce(sq, stream=stream)
+        comm.all_reduce(sq, stream=stream, consumer=plan.handle)
         plan.set_clip(1.0, 1e-6, sq, out=out)
         adam()
 
@@ -437,7 +439,8 @@ def zero_clip_path_rows(n_params, dev, comm, shard_world=8, iters=20):
                                  "queued ahead, as behind backward)" if spin else "HIP events around the call"),
                       "launches": ("sqnorm_partial_out + all_reduce(partials) + clipped AdamW"
                                    if name == "clip_path_zero_n8" else
-                                   "sqnorm (in-kernel combine) + all_reduce(scalar) + clipped AdamW")}
+                                   "sqnorm (in-kernel combine) + all_reduce(scalar) + clipped AdamW"),
+                      "watchdog_mark": "the all-reduce's, on the update kernel's stop event (gs_allreduce_marked)"}
     plan.set_clip(None)
     rows["clip_path_zero_n8"]["vs_scalar_form"] = (rows["clip_path_zero_n8_scalar"]["avg_ms"]
                                                    / rows["clip_path_zero_n8"]["avg_ms"])
