@@ -70,6 +70,9 @@ namespace {
 std::mutex g_live_mu;
 std::vector<gs_comm*> g_live;
 bool comm_live_locked(gs_comm* c) { return std::find(g_live.begin(), g_live.end(), c) != g_live.end(); }
+// the streams of destroyed communicators (until a new stream reuses the handle): a plan
+// whose last launch ran on one must not record its ordering event there (stream_destroyed)
+std::vector<void*> g_dead_streams;
 
 int rccl_fail(ncclResult_t r, const char* what) {
   return fail(GS_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
@@ -322,6 +325,12 @@ int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_
   return comm_track_locked(c, stream);
 }
 
+bool stream_destroyed(void* stream) {
+  if (!stream) return false;
+  std::lock_guard<std::mutex> live(g_live_mu);
+  return std::find(g_dead_streams.begin(), g_dead_streams.end(), stream) != g_dead_streams.end();
+}
+
 int comm_mark_take(gs_comm* c, void** ev) {
   *ev = nullptr;
   std::lock_guard<std::mutex> live(g_live_mu);
@@ -416,6 +425,8 @@ int gs_comm_create_ex(int rank, int world, const uint8_t* uid, int device, int m
   {
     std::lock_guard<std::mutex> live(g_live_mu);
     g_live.push_back(c);
+    g_dead_streams.erase(std::remove(g_dead_streams.begin(), g_dead_streams.end(), static_cast<void*>(c->stream)),
+                         g_dead_streams.end());
   }
   *out = c;
   return GS_OK;
@@ -437,7 +448,13 @@ int gs_comm_destroy(gs_comm* c) {
   for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : c->mark_ring) (void)hipEventDestroy(ev);
   if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream) {
+    {
+      std::lock_guard<std::mutex> live(g_live_mu);
+      g_dead_streams.push_back(c->stream);
+    }
+    (void)hipStreamDestroy(c->stream);
+  }
   delete c;
   return GS_OK;
 }

@@ -282,6 +282,9 @@ int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, d
 // pooled packet after the launch instead).  comm_mark_commit hands the carried event
 // (or that packet) to the watchdog.
 int comm_mark_take(gs_comm* c, void** ev);
+// a destroyed communicator's stream (its work finished before the destroy, which
+// synchronises it): a plan whose last launch ran there records nothing on it
+bool stream_destroyed(void* stream);
 int comm_mark_commit(gs_comm* c, void* ev, void* stream);
 
 // HIP-side implementations (gs_kernels.hip)

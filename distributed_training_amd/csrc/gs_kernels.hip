@@ -123,7 +123,8 @@ int hip_plan_release(gs_plan* p) {
   (void)hip_plan_timer_enable(p, 0);
   // make sure nothing in flight still reads the tables: an event behind the plan's
   // last launch (hipFree below synchronises the device as well, hip_runtime_api.h)
-  if (p->last_event && p->last_stream != nullptr && !p->last_captured && !stream_capturing(p->last_stream) &&
+  if (p->last_event && p->last_stream != nullptr && !stream_destroyed(p->last_stream) && !p->last_captured &&
+      !stream_capturing(p->last_stream) &&
       hipEventRecord(static_cast<hipEvent_t>(p->last_event), static_cast<hipStream_t>(p->last_stream)) ==
           hipSuccess)
     (void)hipEventSynchronize(static_cast<hipEvent_t>(p->last_event));
@@ -181,6 +182,7 @@ int hip_plan_flush(gs_plan* p, void* stream) {
   // per launch cost ~4.7 µs of stream time, scripts/micro/event_chain.hip): it
   // follows everything enqueued there so far, the plan's last launch included.  A
   // previous stream that entered or left a capture since cannot order this launch.
+  if (p->last_stream != nullptr && stream_destroyed(p->last_stream)) p->last_stream = nullptr;  // nothing pending there
   if (p->last_stream != nullptr && p->last_stream != stream && capturing == p->last_captured &&
       (!capturing || cid == p->table_capture_id) &&
       stream_capturing(p->last_stream) == p->last_captured) {

@@ -119,6 +119,52 @@ def test_ddp_full_size_ws1(cuda_device, rccl_pg, model_name):
     assert len(ddp.bucket_indices()) == (5 if model_name == "resnet50" else 10)
 
 
+@pytest.mark.parametrize("div", [3.0, 8.0])
+def test_ddp_full_size_in_step_scale(cuda_device, rccl_pg, div):
+    """The fused 1/world_size scale inside the real step (at ws=1 the
+    pack multiplies by 1.0): ResNet-50 at BASELINE size through the C++ hooks, pack ->
+    RCCL -> unpack on the comm / producer streams, with the packs' divisor set to 3 and
+    8 (what ws=3 / ws=8 pack with, gs_bucketer_set_div_factor): every averaged grad ==
+    local grad * float(1/div) bit for bit (torch's at::mul_out(bucket, grad,
+    1/div_factor) in fp32), and the fused SGD step on those grads == the oracle."""
+    from distributed_training_amd import DistributedDataParallel, FusedSGD
+    from distributed_training_amd.resnet import MODELS
+
+    torch.manual_seed(0)
+    model = MODELS["resnet50"]().to(cuda_device).to(memory_format=torch.channels_last)
+    params = list(model.parameters())
+    local = {}
+    _snap_hooks(params, local)
+    ddp = DistributedDataParallel(model)
+    opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.0, weight_decay=1e-4)
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    inv = float(np.float32(1.0 / div))
+    for it in range(3):  # iteration 0: one bucket; then the rebuilt layout
+        ddp._set_div_factor(div if it > 0 else 1.0)
+        x = torch.rand(4, 3, 224, 224, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (4,), device=cuda_device, generator=g)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = torch.nn.functional.cross_entropy(ddp(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        if it > 0:
+            assert ddp._native_on  # the C++ hooks, the production path
+            for i, p in enumerate(params):
+                want = local[i] * torch.tensor(inv, dtype=torch.float32, device=cuda_device)
+                assert torch.equal(p.grad, want), f"iter {it} param {i}"
+            ref = [O.sgd(to_np(p).reshape(-1), to_np(p.grad).reshape(-1), None, 0.1, 0.0, 0.0, 1e-4, False, False,
+                         True) for p in params]
+            saved = [p.detach().clone() for p in params]
+            opt.step()
+            torch.cuda.synchronize()
+            for i, p in enumerate(params):
+                assert np.array_equal(to_np(p).reshape(-1), ref[i][0]), f"iter {it} param {i} weights"
+                p.data.copy_(saved[i])  # keep the weights: the next iteration's grads stay comparable
+        opt.zero_grad()
+    assert len(ddp.bucket_indices()) == 5
+    ddp.close()
+
+
 def test_ddp_ws1_adam_matches_torch_adam(cuda_device, rccl_pg):
     from distributed_training_amd import DistributedDataParallel, FusedAdam
     from distributed_training_amd.resnet import micro_resnet
