@@ -956,7 +956,9 @@ struct UnscaleOp {
 // clipped updates fold them: no combine and no coefficient launch between the Σg²
 // pass and this one).  A coefficient of exactly 1 leaves every element as it is
 // (x * 1 == x, NaN and -0 included), so the grid then exits before any access.
-template <int N, int DT>
+// NT: non-temporal loads of the grads (above the cache size, nt_read_once: the Σg² pass
+// before it could not leave them in the cache either)
+template <int N, int DT, bool NT = false>
 struct ClipScaleOp {
   static constexpr int kN = N;
   static constexpr int kG = GS_G_UNPACK;
@@ -974,7 +976,7 @@ struct ClipScaleOp {
   __device__ bool fast_ok(const TV& v) const { return v.vec(0); }
   template <bool F>
   __device__ void load(const TV& v, int64_t e0, uint32_t lo, Frag& f) const {
-    ld<DT, N, F>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
+    ld<DT, N, F, NT>(v.ptr[0], e0, lo, v.numel, v.vec(0), f.x);
   }
   template <bool F>
   __device__ void apply(const TV& v, int64_t e0, uint32_t lo, Frag& f, float&) const {
@@ -1152,8 +1154,8 @@ __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
 }
-template <int N, int DT>
-__device__ __forceinline__ void load_hyper(ClipScaleOp<N, DT>& op) {
+template <int N, int DT, bool NT>
+__device__ __forceinline__ void load_hyper(ClipScaleOp<N, DT, NT>& op) {
   op.gsv = clip_multiplier(op.clip, nullptr);
 }
 template <int N, int GD, int LD, bool NTG>

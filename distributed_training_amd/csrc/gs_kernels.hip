@@ -417,15 +417,21 @@ int hip_adam_hyper(double* step, const double* lr, double beta1, double beta2, d
   return GS_OK;
 }
 
-int hip_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream) {
-  DeviceGuard g(p->device);
+template <bool NT>
+static int clip_scale_nt(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream) {
   GS_DISPATCH_FLOAT(dt, DT, {
-    ClipScaleOp<kUnit, DT> op;
+    ClipScaleOp<kUnit, DT, NT> op;
     op.slot = slot;
     op.clip = clip;
     return launch(p, op, stream);
   });
   return GS_OK;
+}
+
+int hip_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream) {
+  DeviceGuard g(p->device);
+  return nt_read_once(p->elems * dtype_bytes(dt)) ? clip_scale_nt<true>(p, slot, dt, clip, stream)
+                                                   : clip_scale_nt<false>(p, slot, dt, clip, stream);
 }
 
 int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* found,
