@@ -140,11 +140,13 @@ def test_ddp_full_size_in_step_scale(cuda_device, rccl_pg, div):
     g = torch.Generator(device=cuda_device).manual_seed(5)
     inv = float(np.float32(1.0 / div))
     for it in range(3):  # iteration 0: one bucket; then the rebuilt layout
-        ddp._set_div_factor(div if it > 0 else 1.0)
         x = torch.rand(4, 3, 224, 224, device=cuda_device, generator=g).to(memory_format=torch.channels_last)
         y = torch.randint(0, 1000, (4,), device=cuda_device, generator=g)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             loss = torch.nn.functional.cross_entropy(ddp(x), y)
+        # the forward sets the divisor for its backward (world size, or the ranks still
+        # training under join): override it between the forward and the backward
+        ddp._set_div_factor(div if it > 0 else 1.0)
         loss.backward()
         torch.cuda.synchronize()
         if it > 0:
