@@ -661,6 +661,10 @@ def _engine_comm(ddp, zero):
 #   * gloo (the rehearsal: N ranks share the box's GPUs): every rank's GPU work
 #     serialises on the shared device — the base times the ranks per GPU — plus the same
 #     per-rank growth.
+# Both scale with the per-rank batch (the base is 256 images a rank).  Checked against
+# the 8-rank rehearsal of the driver's command (gloo, 64 images a rank, round 6,
+# profiles/r6/r6n8_n8_gloo.json): zero2 15.8 s against 63 s estimated, the policy A/B
+# 23.0 s against 166 s, tail / parity / kernel rates 0.4 / 0.6 / 1.4 s against 5-12 s.
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
               "zero2": 2 * 2 * 18.4 / 4,  # at N > 1 two engines (default + overlap_allgather)
               "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0}
@@ -668,10 +672,10 @@ LEG_GROWTH_PER_RANK = 0.10
 LEG_FIXED_PER_RANK_S = {"bucket_policy_ab": 1.0, "zero2": 0.25, "colossal": 0.25, "collective_bench": 0.25}
 
 
-def leg_cost(name, world, backend, ranks_per_gpu=1):
-    """Estimated seconds of leg `name` at `world` ranks (see LEG_COST_S)."""
+def leg_cost(name, world, backend, ranks_per_gpu=1, batch=256):
+    """Estimated seconds of leg `name` at `world` ranks of `batch` images (see LEG_COST_S)."""
     base = LEG_COST_S.get(name, 5.0)
-    share = max(1, ranks_per_gpu) if backend == "gloo" else 1
+    share = (max(1, ranks_per_gpu) if backend == "gloo" else 1) * max(batch, 1) / 256.0
     return max(5.0, base * share * (1.0 + LEG_GROWTH_PER_RANK * (world - 1))
                + LEG_FIXED_PER_RANK_S.get(name, 0.0) * (world - 1))
 
@@ -1508,7 +1512,8 @@ def main():
         if leg_seconds:
             line["leg_seconds"] = dict(leg_seconds)
             line["leg_estimates_s"] = dict(leg_estimates, model="leg_cost(): LEG_COST_S x (ranks per GPU under gloo) "
-                                                               f"x (1 + {LEG_GROWTH_PER_RANK} (N-1)) + per-rank "
+                                                               "x batch / 256 x "
+                                                               f"(1 + {LEG_GROWTH_PER_RANK} (N-1)) + per-rank "
                                                                "communicator set-up")
         if torch_ddp is not None:
             line["torch_ddp"] = torch_ddp
@@ -1542,7 +1547,7 @@ def main():
     leg_estimates: dict = {}
 
     def fits(name):
-        est = leg_cost(name, world, args.pg_backend, ranks_per_gpu)
+        est = leg_cost(name, world, args.pg_backend, ranks_per_gpu, args.batch)
         leg_estimates[name] = round(est, 1)
         if budget <= 0:
             return True

@@ -56,6 +56,9 @@ def test_leg_cost_scales_with_world_size():
             "    c1 = bench.leg_cost(leg, 1, 'nccl')\n"
             "    c8 = bench.leg_cost(leg, 8, 'nccl')\n"
             "    g8 = bench.leg_cost(leg, 8, 'gloo', ranks_per_gpu=8)\n"
+            "    f7 = 7 * bench.LEG_FIXED_PER_RANK_S.get(leg, 0.0)\n"
+            "    assert abs(bench.leg_cost(leg, 8, 'gloo', 8, batch=64) - max(5.0, (g8 - f7) / 4 + f7)) < 1e-9 "
+            "or g8 == 5.0, leg\n"
             "    assert c1 == max(5.0, bench.LEG_COST_S[leg]), leg\n"
             "    assert c8 >= c1 * (1 + 7 * bench.LEG_GROWTH_PER_RANK) - 1e-9 or c8 == 5.0, leg\n"
             "    assert g8 >= 8 * c8 - 8 * 7 * bench.LEG_FIXED_PER_RANK_S.get(leg, 0.0) - 1e-9 or g8 == 5.0, leg\n"
