@@ -505,7 +505,6 @@ __global__ void __launch_bounds__(kCombineBlock) combine_partials(const float* p
 template <class Op>
 __device__ __forceinline__ void chunk_mixed(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
                                             float& acc) {
-  finish_grad_multiplier(op);  // uniform here (a lane may leave below)
   const int64_t e = c * kChunkElems + static_cast<int>(threadIdx.x) * kUnit;
   int lo = t0, hi = t0 + span - 1;
   while (lo < hi) {
@@ -534,7 +533,6 @@ constexpr int kMixedStage = 64;  // tensors per mixed chunk staged (5 KB of LDS)
 template <class Op>
 __device__ __forceinline__ void chunk_mixed_lds(const Op& op, const PlanArgs& P, int t0, int span, int64_t c,
                                                 float& acc, int64_t* s_lo, int64_t* s_hi, TV* s_tv) {
-  finish_grad_multiplier(op);  // uniform here (a lane may leave below)
   __syncthreads();  // the previous mixed chunk's lanes are done with the stage
   if (static_cast<int>(threadIdx.x) < span) {
     const int t = t0 + static_cast<int>(threadIdx.x);
@@ -568,14 +566,12 @@ __device__ __forceinline__ void chunk_full(const Op& op, const PlanArgs& P, int 
   if (op.fast_ok(v)) {
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template load<true>(v, e0, j * kChunkElems + tid * kUnit, f[j]);
-    finish_grad_multiplier(op);
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template apply<true>(v, e0, j * kChunkElems + tid * kUnit, f[j], acc);
   } else {
     // a stream is not 16-B aligned: the checked path over the same range
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template load<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j]);
-    finish_grad_multiplier(op);
 #pragma unroll
     for (int j = 0; j < G; ++j) op.template apply<false>(v, e0 + j * kChunkElems + tid * kUnit, 0u, f[j], acc);
   }
@@ -588,10 +584,7 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
   static_assert(G == 1 || G == 2 || G == 4 || G == 8, "group of 1, 2, 4 or 8 chunks");
   float acc = 0.f;
   load_hyper(op);            // uniform: graph-replayable lr / bias corrections, clip coefficient
-  if (!op.active()) {        // uniform across the grid
-    finish_grad_multiplier(op);  // workgroup 0 still publishes the clip triple
-    return;
-  }
+  if (!op.active()) return;  // uniform across the grid
   __shared__ int64_t s_lo[kMixedStage], s_hi[kMixedStage];  // mixed chunks: the span's extents
   __shared__ TV s_tv[kMixedStage];                            // ... and descriptors
   const int64_t n_groups = (static_cast<int64_t>(P.n_chunks) + G - 1) / G;
@@ -618,7 +611,6 @@ __global__ void __launch_bounds__(kBlock) GS_SGPR_ATTR chunk_kernel(PlanArgs P, 
       else if (cj > 0) chunk_mixed(op, P, tj, cj, c, acc);
     }
   }
-  finish_grad_multiplier(op);  // a workgroup that ran no chunk (workgroup 0 publishes)
   if constexpr (Op::kRed != 0) {
     constexpr bool MAX = Op::kRed == 2;
     const float r = block_reduce<MAX>(acc);
@@ -1012,8 +1004,7 @@ struct SgdOp {
   ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
   bool clip_on = false;
   bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
-  mutable float gsv = 1.f;
-  mutable bool gs_pending = false;  // a folded clip formed after the first loads (GS_FOLD_LATE)
+  float gsv = 1.f;
   struct Frag { float p[N], g[N], b[N]; };
   __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
@@ -1066,8 +1057,7 @@ struct AdamOp {
   ClipArgs clip{};               // folded clip (clip_on), gs_plan_set_clip
   bool clip_on = false;
   bool use_gs = false;           // the grad multiplier gsv applies (set by load_hyper)
-  mutable float gsv = 1.f;
-  mutable bool gs_pending = false;  // a folded clip formed after the first loads (GS_FOLD_LATE)
+  float gsv = 1.f;
   struct Frag { float p[N], g[N], m[N], v[N]; };
   __device__ int phys(int k) const { return k; }
   __device__ bool active() const { return found_inf == nullptr || *found_inf == 0.f; }
@@ -1159,35 +1149,10 @@ __device__ __forceinline__ float clip_multiplier(const ClipArgs& c, const float*
   __syncthreads();
   return s_coef;
 }
-// GS_FOLD_LATE: a folded clip's coefficient is formed after the workgroup's first
-// group of loads is issued (finish_grad_multiplier), so the partial sums' round trip
-// overlaps the data's instead of preceding it; same arithmetic, same bits.
-#ifndef GS_FOLD_LATE
-#define GS_FOLD_LATE 0
-#endif
 template <class Op>
 __device__ __forceinline__ void load_grad_multiplier(Op& op) {
   op.use_gs = op.gscale != nullptr || op.clip_on;
-  if (GS_FOLD_LATE && op.clip_on) {
-    op.gs_pending = true;
-    return;
-  }
   op.gsv = op.clip_on ? clip_multiplier(op.clip, op.gscale) : (op.gscale ? *op.gscale : 1.f);
-}
-// called uniformly by the workgroup (after its first loads, before the first apply,
-// and at its end — workgroup 0 publishes [Σg², coef, ‖g‖] even when it ran no chunk)
-template <class Op, class = void>
-struct has_gs_pending : std::false_type {};
-template <class Op>
-struct has_gs_pending<Op, std::void_t<decltype(std::declval<const Op&>().gs_pending)>> : std::true_type {};
-template <class Op>
-__device__ __forceinline__ void finish_grad_multiplier(const Op& op) {
-  if constexpr (has_gs_pending<Op>::value) {
-    if (op.gs_pending) {
-      op.gsv = clip_multiplier(op.clip, op.gscale);
-      op.gs_pending = false;
-    }
-  }
 }
 template <int N, int DT, bool NT>
 __device__ __forceinline__ void load_hyper(ClipScaleOp<N, DT, NT>& op) {

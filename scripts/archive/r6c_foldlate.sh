@@ -3,7 +3,10 @@
 # (GS_FOLD_LATE=1, a library variant in lib/variants/foldlate/) — first its bit-exactness
 # (the clip-fold, ZeRO-step and kernel tests on the variant), then interleaved with the
 # default over two rounds (scripts/variant_rows.sh): the clip-path rows, configs[3]'s
-# N=8-shard clip path, the tail.
+# N=8-shard clip path, the tail.  The variant was built on the CPU beforehand
+# (make -C distributed_training_amd/csrc OUTDIR=../lib/variants/foldlate
+#  OBJDIR=../../build/gsync_foldlate EXTRA_DEFS=-DGS_FOLD_LATE=1); the option was
+# removed after this A/B lost (profiles/r6/r6c_foldlate_rows.jsonl).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r6c; mkdir -p $OUT
