@@ -667,7 +667,8 @@ def _engine_comm(ddp, zero):
 # 23.0 s against 166 s, tail / parity / kernel rates 0.4 / 0.6 / 1.4 s against 5-12 s.
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
               "zero2": 2 * 2 * 18.4 / 4,  # at N > 1 two engines (default + overlap_allgather)
-              "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0}
+              "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0,
+              "torch_zero2": 15.0, "torch_colossal": 30.0}
 LEG_GROWTH_PER_RANK = 0.10
 LEG_FIXED_PER_RANK_S = {"bucket_policy_ab": 1.0, "zero2": 0.25, "colossal": 0.25, "collective_bench": 0.25}
 
@@ -981,6 +982,26 @@ def colossal_leg(args, world, rank, dev, coll_h, batch=128, steps=8, warmup=8):
     return out
 
 
+def _time_torch_steps(one, world, batch, dev, steps, warmup):
+    """`warmup` untimed steps, then `steps` timed ones bracketed by barrier +
+    synchronize on both sides, MAX over ranks (the headline's bracket)."""
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    return {"images_per_sec": world * batch * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+            "warmup": warmup, "per_gpu_batch": batch,
+            "timing": "barrier + synchronize on both sides, MAX over ranks (as the headline)"}
+
+
 def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
     """The reference's own GPU path beside the headline, in the same run (VERDICT r5
     next 5): a fresh model of the same architecture and seed, torch's
@@ -1007,22 +1028,77 @@ def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    for _ in range(warmup):
-        one()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one()
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    el = float(el.item())
-    out = {"impl": "torch DistributedDataParallel + torch.optim.SGD(foreach), bf16 autocast, channels_last",
-           "images_per_sec": world * args.batch * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
-           "warmup": warmup, "per_gpu_batch": args.batch,
-           "timing": "barrier + synchronize on both sides, MAX over ranks (as the headline)"}
+    out = dict(impl="torch DistributedDataParallel + torch.optim.SGD(foreach), bf16 autocast, channels_last",
+               **_time_torch_steps(one, world, args.batch, dev, steps, warmup))
+    del ddp, opt, model
+    torch.cuda.empty_cache()
+    return out
+
+
+def torch_zero2_leg(args, world, rank, dev, steps=8, warmup=3):
+    """configs[3] on torch alone beside the zero2 leg, same run: FSDP
+    SHARD_GRAD_OP (ZeRO-2: grads reduce-scattered, params replicated) with bf16
+    MixedPrecision over fp32 master params (DeepSpeed's bf16 mode), clip 1.0,
+    torch.optim.AdamW(fused) with the reference's DeepSpeed hyper-parameters
+    (R:resnet/deepspeed/deepspeed_train.py:170-219), ResNet-50 at the zero2 leg's
+    batch and step count."""
+    from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
+
+    from distributed_training_amd.resnet import MODELS
+
+    torch.manual_seed(0)
+    model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    bf = torch.bfloat16
+    fsdp = FSDP(model, sharding_strategy=ShardingStrategy.SHARD_GRAD_OP, device_id=dev,
+                mixed_precision=MixedPrecision(param_dtype=bf, reduce_dtype=bf, buffer_dtype=bf))
+    opt = torch.optim.AdamW(fsdp.parameters(), fused=True, **DS_ADAM)
+    g = torch.Generator(device=dev).manual_seed(4321 + rank)
+    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last).to(bf)
+    y = torch.randint(0, 1000, (args.batch,), device=dev, generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def one():
+        crit(fsdp(x).float(), y).backward()
+        fsdp.clip_grad_norm_(1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    out = dict(impl="torch FSDP(SHARD_GRAD_OP, bf16 MixedPrecision) + clip_grad_norm_(1.0) + "
+                    "torch.optim.AdamW(fused)", **_time_torch_steps(one, world, args.batch, dev, steps, warmup))
+    del fsdp, opt, model
+    torch.cuda.empty_cache()
+    return out
+
+
+def torch_colossal_leg(args, world, rank, dev, batch=128, steps=8, warmup=8):
+    """configs[4] on torch alone beside the colossal leg, same run: what
+    TorchDDPPlugin + mixed_precision='fp16' + HybridAdam run as on torch
+    (R:resnet/colossal/colossal_train.py:118-161): torch DDP, fp16 autocast with
+    the criterion inside, torch.amp.GradScaler, torch.optim.AdamW(fused, lr
+    1e-3 x ws, weight_decay 0), ResNet-152 at the colossal leg's batch."""
+    from distributed_training_amd.resnet import MODELS
+
+    name = "resnet152" if args.model == "resnet50" else args.model
+    torch.manual_seed(0)
+    model = MODELS[name](num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3 * world, weight_decay=0.0, fused=True)
+    scaler = torch.amp.GradScaler("cuda")
+    g = torch.Generator(device=dev).manual_seed(5678 + rank)
+    x = torch.rand(batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (batch,), device=dev, generator=g)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def one():
+        with torch.autocast("cuda", dtype=torch.float16):
+            loss = crit(ddp(x), y)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+        opt.zero_grad(set_to_none=True)
+
+    out = dict(impl="torch DDP + fp16 autocast + torch.amp.GradScaler + torch.optim.AdamW(fused)", model=name,
+               **_time_torch_steps(one, world, batch, dev, steps, warmup))
     del ddp, opt, model
     torch.cuda.empty_cache()
     return out
@@ -1679,6 +1755,17 @@ def main():
         if rank == 0 and torch_ddp is not None:
             print(f"[bench] torch DDP leg: {torch_ddp['images_per_sec']:.1f} images/s "
                   f"(libgsync {img_s:.1f})", file=sys.stderr, flush=True)
+        # configs[3] and configs[4] on torch alone, beside their libgsync legs
+        if zero2 is not None and zero2.get("images_per_sec"):
+            tz = leg("torch_zero2", lambda: torch_zero2_leg(args, world, rank, dev))
+            if tz is not None:
+                zero2["torch"] = tz
+                zero2["vs_torch"] = zero2["images_per_sec"] / tz["images_per_sec"]
+        if colossal is not None and colossal.get("images_per_sec"):
+            tc = leg("torch_colossal", lambda: torch_colossal_leg(args, world, rank, dev, batch=min(128, args.batch)))
+            if tc is not None:
+                colossal["torch"] = tc
+                colossal["vs_torch"] = colossal["images_per_sec"] / tc["images_per_sec"]
     want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
     if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
             and not args.optimizer_overlap):
