@@ -148,7 +148,7 @@ struct AdamHyper {
 struct ClipArgs {
   const float* sq;     // a finished Σg² (groups == 0) or `groups` group sums, `stride` floats apart
   int32_t groups;
-  int32_t stride;      // kRedSyncStride (the plan's own sums) or 1 (gs_plan_set_clip_groups)
+  int32_t stride;      // floats between consecutive group sums (1: contiguous; the plan's own copy and a caller's buffer)
   float max_norm, eps;
   float sq_mul, coef_mul;  // host multipliers (ZeRO's loss scale): 1 = none
   float* out;          // [sq, coef, norm] written by workgroup 0 (nullable)
@@ -309,7 +309,7 @@ int hip_unscale_check(gs_plan* p, int slot, int dt, const float* inv, float* fou
                       void* stream);
 int hip_clip_scale(gs_plan* p, int slot, int dt, const ClipArgs& clip, void* stream);
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream);
-const float* hip_plan_red_groups(const gs_plan* p);  // the 64 group sums of gs_sqnorm_partial
+const float* hip_plan_red_groups(const gs_plan* p);  // the <= 64 group sums of gs_sqnorm_partial, contiguous
 float* hip_plan_red_scalar(const gs_plan* p);        // its finished Σ when red_groups == 0
 int hip_sgd(gs_plan* p, int gdt, int ldt, const SgdHyper& h, const float* gs, const float* fi,
             const ClipArgs* clip, void* stream);

@@ -64,9 +64,10 @@ int hip_plan_upload_static(gs_plan* p) {
   HIP_RET(hipMemset(p->d_table, 0, tb));
   // per-workgroup partials + the fused reduction's counters / group sums (zeroed once;
   // every fused launch leaves them at zero)
-  // (+ one more line: the Σg² scalar of gs_sqnorm_partial when the chunk engine is off)
+  // (+ one more line: the Σg² scalar of gs_sqnorm_partial when the chunk engine is off,
+  // + the contiguous copy of its group sums that a clipped launch folds)
   HIP_RET(hipMalloc(reinterpret_cast<void**>(&p->d_partials),
-                    sizeof(float) * (kGridLimit + kRedSyncWords + kRedSyncStride)));
+                    sizeof(float) * (kGridLimit + kRedSyncWords + kRedSyncStride + GS_RED_PARTIALS)));
   HIP_RET(hipMemset(p->d_partials + kGridLimit, 0, sizeof(float) * kRedSyncWords));
   HIP_RET(hipHostMalloc(&p->pinned, tb * 4, hipHostMallocDefault));
   for (int i = 0; i < 4; ++i) {
@@ -341,8 +342,11 @@ int hip_sqnorm(gs_plan* p, int slot, int dt, float* sq, int acc, void* stream) {
 // (clip_multiplier).  A reduction without the in-kernel combine (GS_RED_FUSE=0)
 // or an empty plan writes the finished Σ into the plan's scalar word instead
 // (red_groups = 0).
+// The group sums as a clipped launch folds them: contiguous, one 256-B run for up to
+// 64 groups (the fused reduction's own copies sit one per 128-B line, beside their
+// counters: a fold over those took 64 lines per workgroup, every workgroup)
 const float* hip_plan_red_groups(const gs_plan* p) {
-  return p->d_partials + kGridLimit + (kRedMaxGroups + 1) * kRedSyncStride;
+  return p->d_partials + kGridLimit + kRedSyncWords + kRedSyncStride;
 }
 float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit + kRedSyncWords; }
 
@@ -353,10 +357,15 @@ float* hip_plan_red_scalar(const gs_plan* p) { return p->d_partials + kGridLimit
 // also contiguous in caller memory, or the finished Σ in groups_out[0].
 int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t* n_groups, void* stream) {
   DeviceGuard g(p->device);
+  // NULL groups_out: the plan's own sums (gs_sqnorm_partial), written contiguously
+  // by the group leaders beside their fused-reduction copies; never the raw form (the
+  // fold must equal gs_sqnorm's combine bit for bit)
+  const bool own = groups_out == nullptr;
+  if (own) groups_out = const_cast<float*>(hip_plan_red_groups(p));
   // caller memory on a small plan (<= 4 Ki chunks: a ZeRO shard at N = 8): one partial per
   // workgroup of a balanced grid, no counters and no combine — the kernel ends with its
   // last store (groups of 8 chunks, one per workgroup, measured 0.7 µs slower: r5f)
-  if (groups_out && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
+  if (!own && !p->chunks.empty() && p->n > 0 && !p->segs.empty() &&
       static_cast<int64_t>(p->chunks.size()) <= kRawChunksMax) {
     GS_TRY_RET(sqnorm_launch(p, slot, dt, groups_out, 0, 2, stream));
     if (n_groups) *n_groups = p->red_groups;
@@ -378,7 +387,7 @@ int hip_sqnorm_partial(gs_plan* p, int slot, int dt, float* groups_out, int32_t*
   p->red_groups = 0;
   if (n_groups) *n_groups = 1;
   GS_TRY_RET(sqnorm_launch(p, slot, dt, hip_plan_red_scalar(p), 0, 0, stream));
-  if (groups_out) {  // the finished Σ in slot 0, the rest of the buffer 0
+  if (!own) {  // the finished Σ in slot 0, the rest of the buffer 0
     HIP_RET(hipMemsetAsync(groups_out, 0, GS_RED_PARTIALS * sizeof(float), static_cast<hipStream_t>(stream)));
     HIP_RET(hipMemcpyAsync(groups_out, hip_plan_red_scalar(p), sizeof(float), hipMemcpyDeviceToDevice,
                            static_cast<hipStream_t>(stream)));

@@ -429,7 +429,7 @@ static int plan_clip(gs_plan* p, ClipArgs* c, const ClipArgs** out) {
       if (p->red_groups > kRedMaxGroups)
         return fail(GS_ESTATE, "clipped update from the plan's own Σg²: more group sums than the plan keeps");
       c->groups = p->red_groups;
-      c->stride = kRedSyncStride;
+      c->stride = 1;  // the contiguous copy (hip_plan_red_groups)
       c->sq = p->red_groups > 0 ? hip_plan_red_groups(p) : hip_plan_red_scalar(p);
     }
   }
