@@ -1035,13 +1035,14 @@ def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
     return out
 
 
-def torch_zero2_leg(args, world, rank, dev, steps=8, warmup=3):
+def torch_zero2_leg(args, world, rank, dev, steps=8, warmup=5):
     """configs[3] on torch alone beside the zero2 leg, same run: FSDP
     SHARD_GRAD_OP (ZeRO-2: grads reduce-scattered, params replicated) with bf16
     MixedPrecision over fp32 master params (DeepSpeed's bf16 mode), clip 1.0,
     torch.optim.AdamW(fused) with the reference's DeepSpeed hyper-parameters
     (R:resnet/deepspeed/deepspeed_train.py:170-219), ResNet-50 at the zero2 leg's
-    batch and step count."""
+    batch and step count (two more warm-up steps than libgsync's leg: FSDP's lazy
+    initialisation runs in its first steps)."""
     from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
 
     from distributed_training_amd.resnet import MODELS
@@ -1070,7 +1071,7 @@ def torch_zero2_leg(args, world, rank, dev, steps=8, warmup=3):
     return out
 
 
-def torch_colossal_leg(args, world, rank, dev, batch=128, steps=8, warmup=8):
+def torch_colossal_leg(args, world, rank, dev, batch=128, steps=8, warmup=10):
     """configs[4] on torch alone beside the colossal leg, same run: what
     TorchDDPPlugin + mixed_precision='fp16' + HybridAdam run as on torch
     (R:resnet/colossal/colossal_train.py:118-161): torch DDP, fp16 autocast with
