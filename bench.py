@@ -997,7 +997,16 @@ def _time_torch_steps(one, world, batch, dev, steps, warmup):
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
+    # per-step durations of a few more steps (events on the current stream): a warm-up
+    # that did not settle shows as a trend here
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(4)]
+    for a, b in evs:
+        a.record()
+        one()
+        b.record()
+    torch.cuda.synchronize()
     return {"images_per_sec": world * batch * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+            "after_ms": [round(a.elapsed_time(b), 3) for a, b in evs],
             "warmup": warmup, "per_gpu_batch": batch,
             "timing": "barrier + synchronize on both sides, MAX over ranks (as the headline)"}
 
@@ -1035,14 +1044,14 @@ def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
     return out
 
 
-def torch_zero2_leg(args, world, rank, dev, steps=8, warmup=5):
+def torch_zero2_leg(args, world, rank, dev, steps=20, warmup=5):
     """configs[3] on torch alone beside the zero2 leg, same run: FSDP
     SHARD_GRAD_OP (ZeRO-2: grads reduce-scattered, params replicated) with bf16
     MixedPrecision over fp32 master params (DeepSpeed's bf16 mode), clip 1.0,
     torch.optim.AdamW(fused) with the reference's DeepSpeed hyper-parameters
     (R:resnet/deepspeed/deepspeed_train.py:170-219), ResNet-50 at the zero2 leg's
-    batch and step count (two more warm-up steps than libgsync's leg: FSDP's lazy
-    initialisation runs in its first steps)."""
+    batch, 5 warm-up and 20 timed steps (FSDP's lazy initialisation runs in its first
+    steps; the standalone `bench.py --impl torch --engine zero2` protocol)."""
     from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
 
     from distributed_training_amd.resnet import MODELS
