@@ -668,7 +668,7 @@ def _engine_comm(ddp, zero):
 LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kernel_rates": 20.0,
               "zero2": 2 * 2 * 18.4 / 4,  # at N > 1 two engines (default + overlap_allgather)
               "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0,
-              "torch_zero2": 15.0, "torch_colossal": 30.0}
+              "torch_colossal": 30.0}
 LEG_GROWTH_PER_RANK = 0.10
 LEG_FIXED_PER_RANK_S = {"bucket_policy_ab": 1.0, "zero2": 0.25, "colossal": 0.25, "collective_bench": 0.25}
 
@@ -1040,42 +1040,6 @@ def torch_ddp_leg(args, world, rank, dev, mf, steps=20, warmup=3):
     out = dict(impl="torch DistributedDataParallel + torch.optim.SGD(foreach), bf16 autocast, channels_last",
                **_time_torch_steps(one, world, args.batch, dev, steps, warmup))
     del ddp, opt, model
-    torch.cuda.empty_cache()
-    return out
-
-
-def torch_zero2_leg(args, world, rank, dev, steps=20, warmup=5):
-    """configs[3] on torch alone beside the zero2 leg, same run: FSDP
-    SHARD_GRAD_OP (ZeRO-2: grads reduce-scattered, params replicated) with bf16
-    MixedPrecision over fp32 master params (DeepSpeed's bf16 mode), clip 1.0,
-    torch.optim.AdamW(fused) with the reference's DeepSpeed hyper-parameters
-    (R:resnet/deepspeed/deepspeed_train.py:170-219), ResNet-50 at the zero2 leg's
-    batch, 5 warm-up and 20 timed steps (FSDP's lazy initialisation runs in its first
-    steps; the standalone `bench.py --impl torch --engine zero2` protocol)."""
-    from torch.distributed.fsdp import FullyShardedDataParallel as FSDP, MixedPrecision, ShardingStrategy
-
-    from distributed_training_amd.resnet import MODELS
-
-    torch.manual_seed(0)
-    model = MODELS[args.model](num_classes=1000).to(dev).to(memory_format=torch.channels_last)
-    bf = torch.bfloat16
-    fsdp = FSDP(model, sharding_strategy=ShardingStrategy.SHARD_GRAD_OP, device_id=dev,
-                mixed_precision=MixedPrecision(param_dtype=bf, reduce_dtype=bf, buffer_dtype=bf))
-    opt = torch.optim.AdamW(fsdp.parameters(), fused=True, **DS_ADAM)
-    g = torch.Generator(device=dev).manual_seed(4321 + rank)
-    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=g).to(memory_format=torch.channels_last).to(bf)
-    y = torch.randint(0, 1000, (args.batch,), device=dev, generator=g)
-    crit = torch.nn.CrossEntropyLoss()
-
-    def one():
-        crit(fsdp(x).float(), y).backward()
-        fsdp.clip_grad_norm_(1.0)
-        opt.step()
-        opt.zero_grad(set_to_none=True)
-
-    out = dict(impl="torch FSDP(SHARD_GRAD_OP, bf16 MixedPrecision) + clip_grad_norm_(1.0) + "
-                    "torch.optim.AdamW(fused)", **_time_torch_steps(one, world, args.batch, dev, steps, warmup))
-    del fsdp, opt, model
     torch.cuda.empty_cache()
     return out
 
@@ -1765,12 +1729,10 @@ def main():
         if rank == 0 and torch_ddp is not None:
             print(f"[bench] torch DDP leg: {torch_ddp['images_per_sec']:.1f} images/s "
                   f"(libgsync {img_s:.1f})", file=sys.stderr, flush=True)
-        # configs[3] and configs[4] on torch alone, beside their libgsync legs
-        if zero2 is not None and zero2.get("images_per_sec"):
-            tz = leg("torch_zero2", lambda: torch_zero2_leg(args, world, rank, dev))
-            if tz is not None:
-                zero2["torch"] = tz
-                zero2["vs_torch"] = zero2["images_per_sec"] / tz["images_per_sec"]
+        # configs[4] on torch alone, beside its libgsync leg.  (configs[3]'s torch FSDP
+        # SHARD_GRAD_OP step read 108-110 ms a step inside this process against 81.5 ms
+        # standalone — r6d, r6f against r6e, cause not found — so it is timed standalone:
+        # scripts/r6e_zero2_vs_fsdp.sh)
         if colossal is not None and colossal.get("images_per_sec"):
             tc = leg("torch_colossal", lambda: torch_colossal_leg(args, world, rank, dev, batch=min(128, args.batch)))
             if tc is not None:

@@ -217,10 +217,9 @@ def test_bench_n1_contract(cuda_device):
     fa = c["fused_adam"]
     assert fa["launches"] + fa["skipped_launches"] == c["steps"]
     assert fa["launches"] == 0 or 0 < fa["frac"] < 1.5
-    # configs[3] / configs[4] on torch alone in the same run (FSDP SHARD_GRAD_OP; DDP + GradScaler)
-    for obj in (z, c):
-        assert obj["torch"]["images_per_sec"] > 0 and obj["torch"]["steps"] > 0
-        assert abs(obj["vs_torch"] - obj["images_per_sec"] / obj["torch"]["images_per_sec"]) < 1e-9
+    # configs[4] on torch alone in the same run (torch DDP + GradScaler + fused AdamW)
+    assert c["torch"]["images_per_sec"] > 0 and c["torch"]["steps"] > 0
+    assert abs(c["vs_torch"] - c["images_per_sec"] / c["torch"]["images_per_sec"]) < 1e-9
 
 
 def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
