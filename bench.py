@@ -131,10 +131,10 @@ def parse():
                     help="after the timed region: re-wrap the model with each DDP bucket policy (torch, xgmi, "
                          "last-bucket cap 1 MiB, torch again) and time each, with tail, bus bandwidth and parity "
                          "(-1: only at N > 1 on the DDP engine) — the data for DESIGN §8's policy rule")
-    ap.add_argument("--torch-leg", type=int, default=-1,
+    ap.add_argument("--torch-leg", type=int, default=1,
                     help="after the legs: the reference's own GPU path (torch DDP + torch.optim.SGD foreach) on the "
-                         "same model / batch / step, timed like the headline; vs_baseline = libgsync / it "
-                         "(-1: only at N = 1)")
+                         "same model / batch / step, timed like the headline; vs_baseline = libgsync / it; "
+                         "and configs[4] on torch beside the colossal leg (0: off)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -1722,9 +1722,16 @@ def main():
         if rank == 0 and colossal is not None:
             print(f"[bench] colossal leg: {colossal['images_per_sec']:.1f} images/s, "
                   f"parity {colossal['parity'].get('ok')}", file=sys.stderr, flush=True)
-    want_torch = args.torch_leg == 1 or (args.torch_leg == -1 and world == 1)
-    if (want_torch and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
-            and args.pg_backend == "nccl"):
+    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
+    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
+            and not args.optimizer_overlap):
+        # after every reading of the headline DDP above: it is closed here
+        policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
+        if rank == 0 and policy_ab is not None:
+            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
+    # the torch legs come after the policy A/B: at N > 1 the A/B decides row N1, the
+    # torch legs only set vs_baseline, so a tight budget skips them first
+    if args.torch_leg != 0 and args.impl == "libgsync" and args.engine == "ddp" and not args.graph:
         torch_ddp = leg("torch_ddp", lambda: torch_ddp_leg(args, world, rank, dev, mf))
         if rank == 0 and torch_ddp is not None:
             print(f"[bench] torch DDP leg: {torch_ddp['images_per_sec']:.1f} images/s "
@@ -1738,13 +1745,6 @@ def main():
             if tc is not None:
                 colossal["torch"] = tc
                 colossal["vs_torch"] = colossal["images_per_sec"] / tc["images_per_sec"]
-    want_ab = args.policy_ab == 1 or (args.policy_ab == -1 and world > 1)
-    if (want_ab and args.impl == "libgsync" and args.engine == "ddp" and not args.graph
-            and not args.optimizer_overlap):
-        # after every reading of the headline DDP above: it is closed here
-        policy_ab = leg("bucket_policy_ab", lambda: bucket_policy_ab(model, opt, ddp, x, y, crit, world, dev, args))
-        if rank == 0 and policy_ab is not None:
-            print(f"[bench] bucket policy A/B: decision {policy_ab['decision']}", file=sys.stderr, flush=True)
     current_leg[0] = "done"
     if watchdog is not None:
         watchdog.cancel()

@@ -129,9 +129,10 @@ def _check_line(d, n):
     assert d["n_gpus"] == n and d["steps"] == 3 and d["warmup"] == 2
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["higher_is_better"] is True and d["scaling"] == "weak"
-    if n == 1 and "rehearsal" not in d["config"]:
-        # the reference's own GPU path (torch DDP + torch.optim.SGD foreach) timed in the same run
-        t = d["torch_ddp"]
+    # the reference's own GPU path (torch DDP + torch.optim.SGD foreach) timed in the same run, at every N
+    t = d.get("torch_ddp")
+    assert t is not None or "torch_ddp" in d.get("leg_errors", {}), d.get("leg_errors")
+    if t is not None:
         assert t["images_per_sec"] > 0 and t["steps"] > 0 and d["vs_baseline_basis"]
         assert abs(d["vs_baseline"] - d["value"] / t["images_per_sec"]) <= 1e-9 * d["vs_baseline"]
     else:
@@ -241,6 +242,11 @@ def test_bench_n2_driver_launch_gloo_rehearsal(cuda_device):
     assert z["parity"]["ok"] is True and z["parity"]["world"] == 2, z["parity"]
     c = lines[0]["colossal"]  # BASELINE configs[4] in the same run
     assert c["engine"] == "colossal" and c["images_per_sec"] > 0 and c["parity"]["ok"] is True, c["parity"]
+    # the torch legs at N > 1 too: torch DDP over the same process group beside the headline
+    t = lines[0]["torch_ddp"]
+    assert t["images_per_sec"] > 0 and t["steps"] == 20
+    assert abs(lines[0]["vs_baseline"] - lines[0]["value"] / t["images_per_sec"]) < 1e-9
+    assert c["torch"]["images_per_sec"] > 0
     assert "leg_errors" not in lines[0], lines[0].get("leg_errors")
 
 
@@ -358,7 +364,8 @@ def test_bench_wall_budget_skips_legs_keeps_the_headline(cuda_device):
     d = lines[0]
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0 and d["n_gpus"] == 2
     skipped = {k for k, v in d["leg_errors"].items() if v.startswith("skipped")}
-    assert {"tail_split", "parity", "collective_bench", "zero2", "colossal", "bucket_policy_ab"} <= skipped, skipped
+    assert {"tail_split", "parity", "collective_bench", "zero2", "colossal", "bucket_policy_ab",
+            "torch_ddp"} <= skipped, skipped
     assert "legs_incomplete" not in d
 
 
