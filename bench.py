@@ -670,12 +670,17 @@ LEG_COST_S = {"tail_split": 5.0, "parity": 5.0, "collective_bench": 10.0, "kerne
               "colossal": 2 * 63.6 / 2, "bucket_policy_ab": 2 * 35.0 * 8 / 6 / 2, "torch_ddp": 10.0,
               "torch_colossal": 30.0}
 LEG_GROWTH_PER_RANK = 0.10
+# torch's own DDP over gloo stages every bucket through the host per rank: its legs ran
+# 3.7x / 2.6x their estimates in the 8-rank rehearsal (profiles/r6/r6n8c_n8_gloo.json)
+LEG_GLOO_FACTOR = {"torch_ddp": 4.0, "torch_colossal": 3.0}
 LEG_FIXED_PER_RANK_S = {"bucket_policy_ab": 1.0, "zero2": 0.25, "colossal": 0.25, "collective_bench": 0.25}
 
 
 def leg_cost(name, world, backend, ranks_per_gpu=1, batch=256):
     """Estimated seconds of leg `name` at `world` ranks of `batch` images (see LEG_COST_S)."""
     base = LEG_COST_S.get(name, 5.0)
+    if backend == "gloo":
+        base *= LEG_GLOO_FACTOR.get(name, 1.0)
     share = (max(1, ranks_per_gpu) if backend == "gloo" else 1) * max(batch, 1) / 256.0
     return max(5.0, base * share * (1.0 + LEG_GROWTH_PER_RANK * (world - 1))
                + LEG_FIXED_PER_RANK_S.get(name, 0.0) * (world - 1))

@@ -46,7 +46,19 @@ struct gs_comm {
   struct Inflight {
     hipEvent_t ev;
     std::chrono::steady_clock::time_point t0;
+    bool from_pool = false;  // a caller-list entry whose event the pool owns (a lapsed deferral)
   };
+  // collectives whose mark waits for a consumer plan's next launch (comm_enqueue with a
+  // consumer): untracked until that launch commits its mark — or, if it has not come
+  // within kDeferLimitMs (the host blocked or idle between the collective and its
+  // consumer, e.g. a loss.item() before the next backward), the watchdog records a
+  // packet on the collective's stream itself and times it from the enqueue
+  struct Deferred {
+    const gs_plan* consumer;  // nullptr once that plan is destroyed
+    hipStream_t stream;
+    std::chrono::steady_clock::time_point t0;
+  };
+  std::vector<Deferred> deferred;
   // packets recorded after a collective (comm_track_locked), in enqueue order: retired
   // from the front, so each poll queries the entries it retires and one pending one
   std::deque<Inflight> pooled;
@@ -144,6 +156,10 @@ int64_t now_ns() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// how long a deferred mark may wait for its consumer's launch before the watchdog
+// records a packet for it (at most half the timeout)
+constexpr int64_t kDeferLimitMs = 1000;
+
 // > 0 while a graph capture is being recorded (gs_watchdog_pause): event
 // queries from the watchdog thread are not allowed during a global-mode capture
 std::atomic<int> g_wd_pause{0};
@@ -203,6 +219,33 @@ void watchdog_loop(gs_comm* c) {
                           " ms (timeout " + std::to_string(c->timeout_ms) + " ms); communicator aborted");
       continue;
     }
+    // Deferred marks whose consumer has not launched within kDeferLimitMs: a packet on
+    // the collective's stream now (stream order: it completes only after the
+    // collective), watched from the collective's enqueue like any caller entry
+    if (!c->deferred.empty()) {
+      const int64_t limit = std::min<int64_t>(kDeferLimitMs, c->timeout_ms > 0 ? c->timeout_ms / 2 : kDeferLimitMs);
+      size_t w = 0;
+      for (size_t i = 0; i < c->deferred.size(); ++i) {
+        const gs_comm::Deferred& d = c->deferred[i];
+        const int64_t age = std::chrono::duration_cast<std::chrono::milliseconds>(now - d.t0).count();
+        hipEvent_t ev = nullptr;
+        if (age > limit && !stream_capturing(d.stream)) {
+          if (!c->ev_pool.empty()) {
+            ev = c->ev_pool.back();
+            c->ev_pool.pop_back();
+          } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+          }
+          if (ev && hipEventRecord(ev, d.stream) != hipSuccess) {
+            c->ev_pool.push_back(ev);
+            ev = nullptr;
+          }
+        }
+        if (ev) c->caller.push_back({ev, d.t0, true});
+        else c->deferred[w++] = d;
+      }
+      c->deferred.resize(w);
+    }
     // The callers' events: every entry past the timeout is queried, of the others
     // kQueries a poll in rotation; a completed entry leaves the list.
     constexpr size_t kQueries = 4;
@@ -229,8 +272,10 @@ void watchdog_loop(gs_comm* c) {
     }
     if (aborted) continue;
     size_t w = 0;
-    for (size_t i = 0; i < n; ++i)
+    for (size_t i = 0; i < n; ++i) {
       if (!done[i]) c->caller[w++] = c->caller[i];
+      else if (c->caller[i].from_pool) c->ev_pool.push_back(c->caller[i].ev);
+    }
     c->caller.resize(w);
     c->caller_next = w ? (c->caller_next + kQueries) % w : 0;
   }
@@ -320,6 +365,7 @@ int comm_enqueue(gs_comm* c, hipStream_t stream, const std::function<ncclResult_
   if (consumer && consumer->kind == GS_DEV_HIP && consumer->n > 0 && !consumer->segs.empty() &&
       c->timeout_ms > 0 && !stream_capturing(stream)) {
     consumer->watch_comm = c;
+    c->deferred.push_back({consumer, stream, std::chrono::steady_clock::now()});
     return GS_OK;
   }
   return comm_track_locked(c, stream);
@@ -353,21 +399,48 @@ int comm_mark_take(gs_comm* c, void** ev) {
   return 1;
 }
 
-int comm_mark_commit(gs_comm* c, void* ev, void* stream) {
+int comm_mark_commit(gs_comm* c, void* ev, void* stream, const gs_plan* consumer) {
   std::lock_guard<std::mutex> live(g_live_mu);
   if (!c || !comm_live_locked(c)) return GS_OK;
   hipEvent_t e = static_cast<hipEvent_t>(ev);
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->timeout_ms <= 0) return GS_OK;
-  if (!e) return comm_track_locked(c, static_cast<hipStream_t>(stream));
-  const auto now = std::chrono::steady_clock::now();
+  // the collectives deferred to this consumer: its launch is stream-ordered after them,
+  // so its mark covers them; the clock runs from the oldest one's enqueue
+  auto t0 = std::chrono::steady_clock::now();
+  bool any = false;
+  size_t w = 0;
+  for (size_t i = 0; i < c->deferred.size(); ++i) {
+    if (c->deferred[i].consumer == consumer) {
+      t0 = std::min(t0, c->deferred[i].t0);
+      any = true;
+    } else {
+      c->deferred[w++] = c->deferred[i];
+    }
+  }
+  c->deferred.resize(w);
+  if (!any) return GS_OK;  // the watchdog already recorded their packets
+  if (!e) {
+    GS_TRY_RET(comm_track_locked(c, static_cast<hipStream_t>(stream)));
+    c->pooled.back().t0 = t0;
+    return GS_OK;
+  }
   for (auto& f : c->caller)
     if (f.ev == e) {
-      f.t0 = now;
+      f.t0 = t0;
       return GS_OK;
     }
-  c->caller.push_back({e, now});
+  c->caller.push_back({e, t0});
   return GS_OK;
+}
+
+void comm_forget_consumer(const gs_plan* consumer) {
+  std::lock_guard<std::mutex> live(g_live_mu);
+  for (gs_comm* c : g_live) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (auto& d : c->deferred)
+      if (d.consumer == consumer) d.consumer = nullptr;  // the watchdog's packet covers it
+  }
 }
 
 }  // namespace gs
@@ -445,6 +518,8 @@ int gs_comm_destroy(gs_comm* c) {
   (void)hipSetDevice(c->device);
   if (c->stream && !c->aborted.load()) (void)hipStreamSynchronize(c->stream);
   for (auto& f : c->pooled) (void)hipEventDestroy(f.ev);  // the caller's events stay the caller's
+  for (auto& f : c->caller)
+    if (f.from_pool) (void)hipEventDestroy(f.ev);  // ... but a lapsed deferral's packet is ours
   for (hipEvent_t ev : c->ev_pool) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : c->mark_ring) (void)hipEventDestroy(ev);
   if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);

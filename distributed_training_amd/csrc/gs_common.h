@@ -285,7 +285,12 @@ int comm_mark_take(gs_comm* c, void** ev);
 // a destroyed communicator's stream (its work finished before the destroy, which
 // synchronises it): a plan whose last launch ran there records nothing on it
 bool stream_destroyed(void* stream);
-int comm_mark_commit(gs_comm* c, void* ev, void* stream);
+// consumer: the launching plan — the collectives deferred to it are covered by its mark,
+// timed from the oldest one's enqueue (a deferral whose consumer has not launched within
+// about a second gets a packet from the watchdog instead)
+int comm_mark_commit(gs_comm* c, void* ev, void* stream, const gs_plan* consumer);
+// a plan being destroyed: collectives deferred to it keep only the watchdog's packet
+void comm_forget_consumer(const gs_plan* consumer);
 
 // HIP-side implementations (gs_kernels.hip)
 int hip_plan_upload_static(gs_plan* p);

@@ -1310,7 +1310,7 @@ int launch(gs_plan* p, Op op, void* stream, float* red_out = nullptr, int accumu
   }
   if (wtake) {
     if (wev && !wcarry) HIP_RET(hipEventRecord(static_cast<hipEvent_t>(wev), s));
-    GS_TRY_RET(comm_mark_commit(wc, wev, stream));
+    GS_TRY_RET(comm_mark_commit(wc, wev, stream, p));
   }
   if (nslots) {
     p->timer_kind[tk] = Op::kKind;

@@ -238,7 +238,10 @@ int gs_plan_create_ex(int device_kind, int device, int n_tensors, const int64_t*
 
 int gs_plan_destroy(gs_plan* p) {
   if (!p) return GS_OK;
-  if (p->kind == GS_DEV_HIP) hip_plan_release(p);
+  if (p->kind == GS_DEV_HIP) {
+    comm_forget_consumer(p);
+    hip_plan_release(p);
+  }
   delete p;
   return GS_OK;
 }

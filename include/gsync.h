@@ -146,6 +146,9 @@ int gs_all_gather(gs_comm* c, const void* send, void* recv, int64_t send_count, 
  * to the watchdog.  The caller guarantees that launch is stream-ordered after
  * the collective (ZeRO: the partials all-reduce before the clipped update on the
  * same stream; the parameter all-gather before the next backward's first pack).
+ * If that launch has not come within half the timeout (at most 1 s), the watchdog
+ * records a packet on `stream` itself and times the collective from its enqueue, so
+ * `stream` must outlive that window (as a plan's last stream, gs_plan_destroy).
  * NULL consumer (or an empty plan, a capture): a packet, as the entry points above.
  * replaces: ProcessGroupNCCL's per-work end event (T:.../ProcessGroupNCCL.hpp:424
  *           ncclEndEvent_), recorded after every collective */

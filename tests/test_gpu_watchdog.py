@@ -9,6 +9,8 @@ on kernels instead of event packets, and stalls that must still abort.
   aborted within the timeout — ZeRO (its reduce-scatter's mark on the update)
   and DDP with more buckets than the watchdog queries per poll (the overdue
   entry is found while the others rotate), each on a private communicator.
+* A deferred mark whose consumer never launches gets the watchdog's own packet
+  after half the timeout (at most 1 s), so a stall there still aborts.
 
 The stall is a spin kernel (torch.cuda._sleep) ahead of the step on its stream;
 with one rank RCCL's collectives touch only the caller's buffers, and the
@@ -125,6 +127,41 @@ def test_zero_stalled_collective_aborts(cuda_device, rccl_pg):
         comm.all_reduce(torch.ones(4, device=cuda_device))
     z.close()
     comm.close()
+
+
+def test_deferred_mark_without_consumer_launch_aborts(cuda_device, rccl_pg):
+    """A collective whose mark is deferred to a consumer plan that never launches
+    (the host blocked or idle between them — a loss.item() before the next
+    backward) is still watched: past about half the timeout the watchdog records
+    a packet on the collective's stream itself, timed from the enqueue, and a
+    stall aborts within the timeout.  Without a stall the packet completes and
+    nothing aborts."""
+    from distributed_training_amd import _lib as L
+    from distributed_training_amd.comm import Communicator
+    from distributed_training_amd.multi_tensor import TensorListPlan
+
+    plan = TensorListPlan([4096], cuda_device)
+    buf = torch.ones(1024, device=cuda_device)
+    stream = torch.cuda.current_stream(cuda_device).cuda_stream
+    # no stall: the lapsed deferral's packet completes, no abort
+    ok = Communicator(None, cuda_device, timeout_ms=400)
+    ok.all_reduce(buf, stream=stream, consumer=plan.handle)
+    torch.cuda.synchronize()
+    time.sleep(1.0)
+    assert ok.status() == (False, "")
+    ok.close()
+    # the stall: the collective queued behind a 2 s kernel, its consumer never launched
+    comm = Communicator(None, cuda_device, timeout_ms=400)
+    torch.cuda._sleep(_spin_cycles(2.0))
+    comm.all_reduce(buf, stream=stream, consumer=plan.handle)
+    time.sleep(1.2)
+    aborted, why = comm.status()
+    assert aborted and "in flight" in why, why
+    torch.cuda.synchronize()
+    with pytest.raises(L.GsyncError, match="aborted"):
+        comm.all_reduce(buf)
+    comm.close()
+    del plan
 
 
 def test_ddp_stall_many_buckets_aborts(cuda_device, rccl_pg):
