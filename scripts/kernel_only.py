@@ -5,7 +5,8 @@ op: sgd | adam (update plan, as FusedSGD / FusedAdam build it), clipsgd (the fol
     path on the update plan: gs_sqnorm_partial + the clipped SGD, max_norm 1.0),
     pack | pack16 | pack16b | unpack | unpacksq | sqnorm | sqpart (bucket-layout plan, align 64;
     pack16 = fp32 grads -> bf16 bucket, pack16b = bf16 grads -> bf16 bucket (ZeRO-2's pack);
-    sqpart = gs_sqnorm_partial, the folded clip's Σg² launch)."""
+    sqpart = gs_sqnorm_partial, the folded clip's Σg² launch; clipscale = clip_grad_norm_'s scale
+    pass, gs_clip_scale, at a fixed coefficient 0.1 so every launch writes)."""
 import os
 import sys
 
@@ -36,6 +37,7 @@ else:
     plan.set_ptrs(1, gs)
     flat = torch.zeros(plan.flat_numel, device=dev, dtype=torch.bfloat16 if op in ("pack16", "pack16b") else torch.float32)
     sq = torch.zeros(1, device=dev)
+    sq100 = torch.full((1,), 100.0, device=dev)  # clipscale: ||g|| = 10, max_norm 1 -> coefficient ~0.1
 for _ in range(iters):
     if op == "adam":
         plan.adam(torch.float32, 1e-6, 0.9, 0.999, 1e-8, 0.0, False, False, -1e-6, 0.5)
@@ -55,5 +57,8 @@ for _ in range(iters):
         plan.sqnorm(1, torch.float32, sq)
     elif op == "sqpart":
         plan.sqnorm_partial(1, torch.float32)
+    elif op == "clipscale":
+        plan.set_clip(1.0, 1e-6, sq100)
+        plan.clip_scale(1, torch.float32)
 torch.cuda.synchronize()
 print("params", sum(n), "launches", iters, "op", op)

@@ -12,7 +12,7 @@ import sys
 
 KERNEL = {"sgd": "SgdOp", "adam": "AdamOp", "pack": "PackOp", "pack16": "PackOp", "pack16b": "PackOp", "unpack": "UnpackOp",
           "unpacksq": "UnpackOp", "sqnorm": "SqnormOp", "sqpart": "SqnormOp",
-          "clipsgd": "SgdOp"}  # clipsgd: the clipped update's own dispatches (its Σg² launch is sqpart)
+          "clipsgd": "SgdOp", "clipscale": "ClipScaleOp"}  # clipsgd: the clipped update's own dispatches (its Σg² launch is sqpart)
 
 
 def load(d, counter, tag="SgdOp"):
