@@ -62,6 +62,11 @@ def test_leg_cost_scales_with_world_size():
             "    assert c1 == max(5.0, bench.LEG_COST_S[leg]), leg\n"
             "    assert c8 >= c1 * (1 + 7 * bench.LEG_GROWTH_PER_RANK) - 1e-9 or c8 == 5.0, leg\n"
             "    assert g8 >= 8 * c8 - 8 * 7 * bench.LEG_FIXED_PER_RANK_S.get(leg, 0.0) - 1e-9 or g8 == 5.0, leg\n"
+            "# torch's own DDP legs stage through the host under gloo (the 8-rank rehearsal, r6n8c)\n"
+            "for leg, f in bench.LEG_GLOO_FACTOR.items():\n"
+            "    assert f >= 1 and leg in bench.LEG_COST_S, leg\n"
+            "    assert abs(bench.leg_cost(leg, 8, 'gloo', 8, batch=64) - f * bench.LEG_COST_S[leg] * 2 * 1.7) < 1e-9, leg\n"
+            "    assert abs(bench.leg_cost(leg, 8, 'nccl') - bench.LEG_COST_S[leg] * 1.7) < 1e-9, leg\n"
             "print('ok')" % REPO)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]
