@@ -325,10 +325,12 @@ def test_bench_multirank_gloo_rehearsal(cuda_device, engine, n):
     """More ranks than the N=2 rehearsal, as the driver's 4/8-GPU runs: DDP at 4
     ranks (the parity step's ws > 2 tolerance path, rank order != the
     collective's order) and ZeRO-2 at 3 ranks (shards of a flat buffer padded
-    to 3 x 64 elements; reduce-scatter / all-gather over the rehearsal group)."""
+    to 3 x 64 elements; reduce-scatter / all-gather over the rehearsal group).  No torch
+    legs: torch's own DDP over gloo stages every bucket through the host and alone
+    takes most of the child's time limit at 4 ranks (the N=2 rehearsal runs them)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           "bench.py", "--gpus", str(n), "--pg-backend", "gloo", "--kernel-rates", "0"] + SMALL + NO_LEGS
+           "bench.py", "--gpus", str(n), "--pg-backend", "gloo", "--kernel-rates", "0", "--torch-leg", "0"] + SMALL + NO_LEGS
     if engine == "zero2":
         cmd += ["--engine", "zero2"]
     # a healthy run takes ~30 s; a hung one dumps every rank's stacks each 40 s into the stderr file
