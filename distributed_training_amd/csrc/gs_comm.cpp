@@ -421,8 +421,11 @@ int comm_mark_commit(gs_comm* c, void* ev, void* stream, const gs_plan* consumer
   c->deferred.resize(w);
   if (!any) return GS_OK;  // the watchdog already recorded their packets
   if (!e) {
+    // the packet joins the FIFO behind younger entries with its older clock: it is timed
+    // once it reaches the front, at most the deferral window (<= 1 s) late
+    const size_t before = c->pooled.size();
     GS_TRY_RET(comm_track_locked(c, static_cast<hipStream_t>(stream)));
-    c->pooled.back().t0 = t0;
+    if (c->pooled.size() > before) c->pooled.back().t0 = t0;
     return GS_OK;
   }
   for (auto& f : c->caller)
